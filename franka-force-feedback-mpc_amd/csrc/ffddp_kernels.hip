@@ -1,0 +1,1373 @@
+// ffddp_kernels.hip — batched (Box)FDDP on MI355X (gfx950), fp64.
+//
+// One solve() of crocoddyl::SolverBoxFDDP (reference call sites
+// crocoddyl_classical.py:367 / crocoddyl_force_feedback.py:605) for B
+// independent OCP instances, as a fixed sequence of kernels per FDDP
+// iteration; all per-instance control flow (regularisation, line-search
+// acceptance, feasibility, stopping) lives on the device, masked per instance:
+//
+//   k_node      calc + calcDiff of every (instance, node):  16-lane group per
+//               node, lane j carries forward-mode direction j (Jacobian column
+//               j), Gauss-Newton Hessians assembled across the group in LDS.
+//   k_backward  Riccati backward pass, one wavefront per instance, blocks in
+//               LDS; Cholesky (infeasible iterations) or BoxQP gains;
+//               regularisation retries inside the kernel.
+//   k_forward   line search: one lane per (instance, step length) — the ten
+//               trials of SolverFDDP::solve evaluated concurrently (the first
+//               accepted one is the sequential answer).
+//   k_accept    acceptance test / regularisation / stopping (SolverFDDP::solve).
+//   k_commit    copy the accepted trial into (xs, us).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ffddp_node.hpp"
+
+using namespace ffddp;
+
+namespace {
+
+constexpr int NODE_GROUP = 16;
+constexpr int NODE_BLOCK = 256;
+constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
+constexpr int BW_BLOCK = 64;
+constexpr int FW_BLOCK = 64;
+
+struct InstState {
+  double preg, cost, dg, dq, stop;
+  int is_feasible, was_feasible, done, ok, iter, recalc, accepted, bw_ok;
+  int n_iters, n_trials, n_retries, n_backward;
+};
+
+struct Dev {
+  int B, N, nx, rec;
+  double* rec_buf;   // [B][N+1][rec]
+  double* fs;        // [B][N+1][nx]
+  double* xs;        // [B][N+1][nx]
+  double* us;        // [B][N][7]
+  double* K;         // [B][N][7][nx]
+  double* k;         // [B][N][7]
+  double* w;         // [B][N+1][nx]   Vxx_t fs_t
+  double* xs_try;    // [B][T][N+1][nx]
+  double* us_try;    // [B][T][N][7]
+  double* trial;     // [B][T][2]  cost_try, dv
+  int* trial_fail;   // [B][T]
+  InstState* st;     // [B]
+};
+
+// ---------------------------------------------------------------------------
+// init
+// ---------------------------------------------------------------------------
+__global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __restrict__ xs_init,
+                       const double* __restrict__ us_init, int is_feasible) {
+  const DevConsts& C = *Cg;
+  const int N = C.N, nx = C.nx;
+  const long nX = (long)d.B * (N + 1) * nx;
+  const long nU = (long)d.B * N * NU;
+  const long nK = (long)d.B * N * NU * nx;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nK; i += (long)gridDim.x * blockDim.x) {
+    if (i < nX) d.xs[i] = xs_init[i];
+    if (i < nU) {
+      d.us[i] = us_init[i];
+      d.k[i] = 0.0;
+    }
+    d.K[i] = 0.0;
+    if (i < d.B) {
+      InstState s;
+      s.preg = C.reg_min;
+      s.cost = 0.0;
+      s.dg = s.dq = 0.0;
+      s.stop = __builtin_nan("");
+      s.is_feasible = is_feasible;
+      s.was_feasible = 0;
+      s.done = 0;
+      s.ok = 0;
+      s.iter = 0;
+      s.recalc = 1;
+      s.accepted = -1;
+      s.bw_ok = 0;
+      s.n_iters = s.n_trials = s.n_retries = s.n_backward = 0;
+      d.st[i] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// calc + calcDiff of all nodes
+// ---------------------------------------------------------------------------
+struct NodeShared {
+  Primal P[NODE_GPB];
+  double col[NODE_GPB][14][NDENSE_MAX];  // residual-Jacobian columns, state directions
+  double colu[NODE_GPB][7][FFDDP_MAX_NC];  // force rows, inner-control directions
+};
+
+template <int NC, bool FF>
+__global__ __launch_bounds__(NODE_BLOCK) void k_node(const DevConsts* __restrict__ Cg, Dev d,
+                                                      const double* __restrict__ x0,
+                                                      const double* __restrict__ node_ref,
+                                                      const double* __restrict__ inst_ref,
+                                                      const uint8_t* __restrict__ surface, int force_all) {
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  constexpr int nx = FF ? 21 : 14;
+  constexpr int nc = NC;
+  __shared__ NodeShared S;
+  const int grp = threadIdx.x / NODE_GROUP, lane = threadIdx.x % NODE_GROUP;
+  const long node = (long)blockIdx.x * NODE_GPB + grp;
+  const int b = (int)(node / (N + 1)), t = (int)(node % (N + 1));
+  bool active = b < d.B;
+  if (active && !force_all) active = (d.st[b].done == 0) && (d.st[b].recalc != 0);
+  const bool surf = active ? surface[b] != 0 : false;
+  const bool terminal = t == N;
+  constexpr bool ff = FF;
+  const int mode = !terminal ? MODE_RUNNING : (ff ? MODE_TERMINAL_U : MODE_TERMINAL_X);
+  const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
+  const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
+  const double* xreg = inst_ref + (long)b * 21;
+  const double* tauref = xreg + 14;
+  // inner control: classical u_t, FF tau = y[14:21]
+  const double* uin = ff ? (y + 14) : (terminal ? nullptr : d.us + ((long)b * N + t) * NU);
+  Primal& P = S.P[grp];
+  if (active && lane == 0) node_primal<NC>(C, mode, surf, y, uin, ref, xreg, tauref, P);
+  __syncthreads();
+  const bool need_u = mode != MODE_TERMINAL_X;
+  double da[NQ], dlam[3], col[NDENSE_MAX];
+  double dau[NQ], dlamu[3];
+  if (active && lane < 14) {
+    node_tangent_state<NC>(C, mode, surf, y, ref, P, lane, da, dlam, col);
+    for (int r = 0; r < 12 + nc; ++r) S.col[grp][lane][r] = col[r];
+  }
+  if (active && lane < 7 && need_u) {
+    node_tangent_control<NC>(C, surf, P, lane, dau, dlamu);
+    for (int r = 0; r < nc; ++r) S.colu[grp][lane][r] = (surf ? dlamu[r] : 0.0);
+  }
+  __syncthreads();
+  if (active) {
+    double* rec = d.rec_buf + ((long)b * (N + 1) + t) * d.rec;
+    const int nd = 12 + nc;
+    const bool scale = mode != MODE_TERMINAL_X;
+    const double sc = scale ? C.dt : 1.0;
+    const double* D = P.D;
+    const double* g = P.g;
+    if (lane < 14) {
+      const int j = lane;
+      // dynamics Jacobian columns
+      if (need_u)
+        for (int i = 0; i < NQ; ++i) rec[rec_off_A() + j * NQ + i] = da[i];
+      // Lxx_in column j (rows 0..13)
+      double* Lxx = rec + rec_off_Lxx(nx);
+      for (int i = 0; i < 14; ++i) {
+        double acc = 0.0;
+        for (int r = 0; r < nd; ++r) acc += S.col[grp][i][r] * D[r] * col[r];
+        if (i == j) acc += P.Dx[j];
+        acc *= sc;
+        if (ff && i == j) acc += C.w_y * C.Wy2[j];
+        Lxx[i * nx + j] = acc;
+      }
+      // Lx_in[j]
+      double lx = 0.0;
+      for (int r = 0; r < nd; ++r) lx += col[r] * g[r];
+      lx = (lx + P.gx[j]) * sc;
+      if (ff) lx += C.w_y * C.Wy2[j] * (y[j] - x0[(long)b * nx + j]);
+      rec[rec_off_Lx(nx) + j] = lx;
+      // Lxu_in row j (force rows only): classical -> Lxu row j; FF -> Lxx_aug[14+k][j]
+      if (need_u) {
+        for (int kk = 0; kk < NU; ++kk) {
+          double acc = 0.0;
+          for (int r = 0; r < nc; ++r) acc += col[12 + r] * D[12 + r] * S.colu[grp][kk][r];
+          acc *= sc;
+          if (ff)
+            Lxx[(14 + kk) * nx + j] = acc;
+          else
+            rec[rec_off_Lxu(nx) + j * NU + kk] = acc;
+        }
+      }
+    }
+    if (lane < 7 && need_u) {
+      const int kk = lane;
+      for (int i = 0; i < NQ; ++i) rec[rec_off_A() + (14 + kk) * NQ + i] = dau[i];
+      // Luu_in column kk
+      double luu[7];
+      for (int m = 0; m < NU; ++m) {
+        double acc = 0.0;
+        for (int r = 0; r < nc; ++r) acc += S.colu[grp][m][r] * D[12 + r] * S.colu[grp][kk][r];
+        if (m == kk) acc += P.Du[kk];
+        luu[m] = acc * sc;
+      }
+      double lu = 0.0;
+      for (int r = 0; r < nc; ++r) lu += S.colu[grp][kk][r] * g[12 + r];
+      lu = (lu + P.gu[kk]) * sc;
+      if (!ff) {
+        for (int m = 0; m < NU; ++m) rec[rec_off_Luu(nx) + m * NU + kk] = luu[m];
+        rec[rec_off_Lu(nx) + kk] = lu;
+      } else {
+        double* Lxx = rec + rec_off_Lxx(nx);
+        // Lxx_aug column 14+kk: rows 0..13 = Lxu_in[:, kk], rows 14..20 = Luu_in[:, kk] + w_y Wy2
+        for (int i = 0; i < 14; ++i) {
+          double acc = 0.0;
+          for (int r = 0; r < nc; ++r) acc += S.col[grp][i][12 + r] * D[12 + r] * S.colu[grp][kk][r];
+          Lxx[i * nx + 14 + kk] = acc * sc;
+        }
+        for (int m = 0; m < NU; ++m)
+          Lxx[(14 + m) * nx + 14 + kk] = luu[m] + (m == kk ? C.w_y * C.Wy2[14 + kk] : 0.0);
+        rec[rec_off_Lx(nx) + 14 + kk] = lu + C.w_y * C.Wy2[14 + kk] * (y[14 + kk] - x0[(long)b * nx + 14 + kk]);
+        // augmented control terms: Lu = w_w w + w_s g_soft ; Luu = diag ; Lxu = 0
+        double wk = 0.0;
+        if (!terminal) wk = d.us[((long)b * N + t) * NU + kk];
+        const double ov = fabs(wk) - C.ws_lim[kk];
+        const bool act = ov > 0.0;
+        const double gs = act ? ov * (wk > 0.0 ? 1.0 : (wk < 0.0 ? -1.0 : 0.0)) : 0.0;
+        rec[rec_off_Lu(nx) + kk] = C.w_w * wk + C.w_ws * gs;
+        for (int m = 0; m < NU; ++m)
+          rec[rec_off_Luu(nx) + m * NU + kk] = (m == kk) ? (C.w_w + C.w_ws * (act ? 1.0 : 0.0)) : 0.0;
+        for (int i = 0; i < nx; ++i) rec[rec_off_Lxu(nx) + i * NU + kk] = 0.0;
+      }
+    }
+    if (!need_u && lane < 7) {
+      // classical terminal: no control blocks (zero them for the calcDiff export)
+      for (int i = 0; i < NQ; ++i) rec[rec_off_A() + (14 + lane) * NQ + i] = 0.0;
+    }
+    if (lane == 15) {
+      // node cost, contact force, gap
+      double cost;
+      if (!ff) {
+        cost = terminal ? P.cost : C.dt * P.cost;
+      } else {
+        const double* tau = y + 14;
+        double wz[7] = {0, 0, 0, 0, 0, 0, 0};
+        const double* ww = terminal ? wz : d.us + ((long)b * N + t) * NU;
+        double c = C.dt * P.cost;
+        if (C.w_y > 0.0) {
+          double a = 0.0;
+          for (int i = 0; i < 21; ++i) {
+            const double dd = y[i] - x0[(long)b * nx + i];
+            a += C.Wy2[i] * dd * dd;
+          }
+          c += 0.5 * C.w_y * a;
+        }
+        if (C.w_w > 0.0) {
+          double a = 0.0;
+          for (int i = 0; i < 7; ++i) a += ww[i] * ww[i];
+          c += 0.5 * C.w_w * a;
+        }
+        if (C.w_ws > 0.0) {
+          double a = 0.0;
+          for (int i = 0; i < 7; ++i) {
+            const double ov = fabs(ww[i]) - C.ws_lim[i];
+            const double o = ov > 0.0 ? ov : 0.0;
+            a += o * o;
+          }
+          c += C.w_ws * (0.5 * a);
+        }
+        cost = c;
+        (void)tau;
+      }
+      rec[rec_off_cost(nx)] = cost;
+      for (int r = 0; r < 3; ++r) rec[rec_off_lam(nx) + r] = (mode == MODE_TERMINAL_X) ? 0.0 : P.lam[r];
+      // gaps fs[t+1] = xnext_t - xs[t+1] ; fs[0] = x0 - xs[0]  (zero once feasible)
+      const bool feas = d.st[b].is_feasible != 0;
+      if (!terminal) {
+        double* f = d.fs + ((long)b * (N + 1) + t + 1) * nx;
+        const double* yn = d.xs + ((long)b * (N + 1) + t + 1) * nx;
+        double xn[21];
+        for (int i = 0; i < 14; ++i) xn[i] = P.xnext[i];
+        if (ff) {
+          const double* wv = d.us + ((long)b * N + t) * NU;
+          for (int i = 0; i < 7; ++i) xn[14 + i] = C.alpha * y[14 + i] + C.beta * wv[i];
+        }
+        for (int i = 0; i < nx; ++i) f[i] = feas ? 0.0 : xn[i] - yn[i];
+      }
+      if (t == 0) {
+        double* f = d.fs + (long)b * (N + 1) * nx;
+        for (int i = 0; i < nx; ++i) f[i] = feas ? 0.0 : x0[(long)b * nx + i] - y[i];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward pass: one wavefront per instance
+// ---------------------------------------------------------------------------
+constexpr int NXM = 21;
+
+struct BwShared {
+  double Vxx[NXM * NXM];
+  double Vx[NXM];
+  double Fx[NXM * NXM];
+  double Fu[NXM * NU];
+  double T1[NXM * NXM];  // Fx^T Vxx'
+  double T2[NU * NXM];   // Fu^T Vxx'
+  double Qxx[NXM * NXM];
+  double Qxu[NXM * NU];
+  double Quu[NU * NU];
+  double Qx[NXM];
+  double Qu[NU];
+  double Qinv[NU * NU];  // Quu^-1 restricted to the free set (BoxQP) / unused for LLT
+  double L[28];
+  double K[NU * NXM];
+  double kk[NU];
+  double fs[NXM];
+  double red[64];
+  int flag;
+  int clamped[NU];
+};
+
+__device__ __forceinline__ bool bad(double v) { return isnan(v) || isinf(v) || v >= 1e30; }
+
+// BoxQP (crocoddyl::BoxQP::solve), single lane.  H 7x7 (row-major), q, lb, ub,
+// x (in: warm start, out: solution), Hinv (free-block inverse scattered into
+// 7x7, zeros elsewhere), clamped flags.  Returns false on LLT failure.
+__device__ bool boxqp(const DevConsts& C, const double* H, const double* q, const double* lb, const double* ub,
+                      double* x, double* Hinv, int* clamped) {
+  for (int i = 0; i < NU; ++i) x[i] = fmax(fmin(x[i], ub[i]), lb[i]);
+  int freeI[NU], nf = NU;
+  for (int it = 0; it < C.qp_maxiter; ++it) {
+    double g[NU];
+    for (int i = 0; i < NU; ++i) {
+      double acc = q[i];
+      for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * x[j];
+      g[i] = acc;
+    }
+    nf = 0;
+    for (int j = 0; j < NU; ++j) {
+      const bool c = (x[j] == lb[j] && g[j] > 0.0) || (x[j] == ub[j] && g[j] < 0.0);
+      clamped[j] = c ? 1 : 0;
+      if (!c) freeI[nf++] = j;
+    }
+    double Lf[28];
+    for (int i = 0; i < nf; ++i)
+      for (int j = 0; j <= i; ++j) Lf[tri(i, j)] = H[freeI[i] * NU + freeI[j]] + ((i == j) ? C.qp_reg : 0.0);
+    // LLT
+    for (int j = 0; j < nf; ++j) {
+      double dd = Lf[tri(j, j)];
+      for (int k = 0; k < j; ++k) dd -= Lf[tri(j, k)] * Lf[tri(j, k)];
+      if (!(dd > 0.0)) return false;
+      const double l = sqrt(dd);
+      Lf[tri(j, j)] = l;
+      for (int i = j + 1; i < nf; ++i) {
+        double s = Lf[tri(i, j)];
+        for (int k = 0; k < j; ++k) s -= Lf[tri(i, k)] * Lf[tri(j, k)];
+        Lf[tri(i, j)] = s / l;
+      }
+    }
+    // Hff^-1 (scattered)
+    for (int i = 0; i < NU * NU; ++i) Hinv[i] = 0.0;
+    for (int c = 0; c < nf; ++c) {
+      double e[NU];
+      for (int i = 0; i < nf; ++i) e[i] = (i == c) ? 1.0 : 0.0;
+      for (int i = 0; i < nf; ++i) {
+        double s = e[i];
+        for (int k = 0; k < i; ++k) s -= Lf[tri(i, k)] * e[k];
+        e[i] = s / Lf[tri(i, i)];
+      }
+      for (int i = nf - 1; i >= 0; --i) {
+        double s = e[i];
+        for (int k = i + 1; k < nf; ++k) s -= Lf[tri(k, i)] * e[k];
+        e[i] = s / Lf[tri(i, i)];
+      }
+      for (int i = 0; i < nf; ++i) Hinv[freeI[i] * NU + freeI[c]] = e[i];
+    }
+    // Newton step on the free set
+    double dxf[NU];
+    for (int i = 0; i < nf; ++i) {
+      double acc = -q[freeI[i]];
+      for (int j = 0; j < NU; ++j)
+        if (clamped[j]) acc -= H[freeI[i] * NU + j] * x[j];
+      dxf[i] = acc;
+    }
+    for (int i = 0; i < nf; ++i) {
+      double s = dxf[i];
+      for (int k = 0; k < i; ++k) s -= Lf[tri(i, k)] * dxf[k];
+      dxf[i] = s / Lf[tri(i, i)];
+    }
+    for (int i = nf - 1; i >= 0; --i) {
+      double s = dxf[i];
+      for (int k = i + 1; k < nf; ++k) s -= Lf[tri(k, i)] * dxf[k];
+      dxf[i] = s / Lf[tri(i, i)];
+    }
+    double dx[NU];
+    for (int i = 0; i < NU; ++i) dx[i] = 0.0;
+    double dmax = 0.0;
+    for (int i = 0; i < nf; ++i) {
+      dx[freeI[i]] = dxf[i] - x[freeI[i]];
+      dmax = fmax(dmax, fabs(dx[freeI[i]]));
+    }
+    if (dmax < C.qp_th_grad) break;
+    double Hx[NU];
+    double fold = 0.0;
+    for (int i = 0; i < NU; ++i) {
+      double acc = 0.0;
+      for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * x[j];
+      Hx[i] = acc;
+    }
+    {
+      double a1 = 0.0, a2 = 0.0;
+      for (int i = 0; i < NU; ++i) {
+        a1 += x[i] * Hx[i];
+        a2 += q[i] * x[i];
+      }
+      fold = 0.5 * a1 + a2;
+    }
+    for (int ia = 0; ia < NTRIALS; ++ia) {
+      const double al = C.alphas[ia];
+      double xn[NU];
+      for (int i = 0; i < NU; ++i) xn[i] = fmax(fmin(x[i] + al * dx[i], ub[i]), lb[i]);
+      double a1 = 0.0, a2 = 0.0, gd = 0.0;
+      for (int i = 0; i < NU; ++i) {
+        double acc = 0.0;
+        for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * xn[j];
+        a1 += xn[i] * acc;
+        a2 += q[i] * xn[i];
+        gd += g[i] * (x[i] - xn[i]);
+      }
+      const double fnew = 0.5 * a1 + a2;
+      if (fold - fnew > C.qp_th_acceptstep * gd) {
+        for (int i = 0; i < NU; ++i) x[i] = xn[i];
+        break;
+      }
+    }
+  }
+  return true;
+}
+
+template <bool FF>
+__global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restrict__ Cg, Dev d, int iter) {
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  constexpr int nx = FF ? 21 : 14;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (b >= d.B) return;
+  InstState* st = d.st + b;
+  if (st->done) return;
+  __shared__ BwShared S;
+  constexpr bool ff = FF;
+  const double dt = C.dt;
+  const bool feas = st->is_feasible != 0;
+  const bool use_qp = C.use_box && feas;
+  const double* recb = d.rec_buf + (long)b * (N + 1) * d.rec;
+  // total cost from the fresh calc (ShootingProblem::calcDiff sum, t = 0..N)
+  if (st->recalc && tid == 0) {
+    double c = 0.0;
+    for (int t = 0; t <= N; ++t) c += recb[(long)t * d.rec + rec_off_cost(nx)];
+    st->cost = c;
+  }
+  double preg = st->preg;
+  int retries = 0;
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) S.flag = 0;
+    // terminal: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N)
+    const double* rT = recb + (long)N * d.rec;
+    const double* fsN = d.fs + ((long)b * (N + 1) + N) * nx;
+    for (int e = tid; e < nx * nx; e += BW_BLOCK) {
+      const int i = e / nx, j = e % nx;
+      S.Vxx[e] = rT[rec_off_Lxx(nx) + e] + (i == j ? preg : 0.0);
+    }
+    for (int i = tid; i < nx; i += BW_BLOCK) S.fs[i] = fsN[i];
+    __syncthreads();
+    double dg = 0.0, dq = 0.0, stop = 0.0;  // lane-0 accumulators
+    for (int i = tid; i < nx; i += BW_BLOCK) {
+      double acc = rT[rec_off_Lx(nx) + i];
+      if (!feas)
+        for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
+      S.Vx[i] = acc;
+    }
+    __syncthreads();
+    // gap terms of the terminal node and w_N = Vxx_N fs_N
+    if (!feas) {
+      double* wN = d.w + ((long)b * (N + 1) + N) * nx;
+      for (int i = tid; i < nx; i += BW_BLOCK) {
+        double acc = 0.0;
+        for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
+        wN[i] = acc;
+      }
+      if (tid == 0) {
+        double a1 = 0.0, a2 = 0.0;
+        for (int i = 0; i < nx; ++i) {
+          double acc = 0.0;
+          for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
+          a1 += S.Vx[i] * S.fs[i];
+          a2 += S.fs[i] * acc;
+        }
+        dg -= a1;
+        dq += a2;
+      }
+    }
+    bool failed = false;
+    for (int t = N - 1; t >= 0; --t) {
+      const double* r = recb + (long)t * d.rec;
+      const double* A = r + rec_off_A();
+      __syncthreads();
+      // Fx, Fu from the node's acceleration Jacobian (IntegratedActionModelEuler::calcDiff)
+      for (int e = tid; e < nx * nx; e += BW_BLOCK) {
+        const int i = e / nx, j = e % nx;
+        double v = (i == j) ? 1.0 : 0.0;
+        if (i < 14 && j < (ff ? 21 : 14)) {
+          const double aij = A[j * NQ + (i % 7)];
+          v += (i < 7 ? dt * dt : dt) * aij;
+          if (i < 7 && j == i + 7) v += dt;
+        }
+        if (ff && i >= 14) v = (i == j) ? C.alpha : 0.0;
+        S.Fx[e] = v;
+      }
+      for (int e = tid; e < nx * NU; e += BW_BLOCK) {
+        const int i = e / NU, kk = e % NU;
+        double v;
+        if (!ff)
+          v = (i < 7 ? dt * dt : dt) * A[(14 + kk) * NQ + (i % 7)];
+        else
+          v = (i >= 14 && i - 14 == kk) ? C.beta : 0.0;
+        S.Fu[e] = v;
+      }
+      const double* fst = d.fs + ((long)b * (N + 1) + t) * nx;
+      for (int i = tid; i < nx; i += BW_BLOCK) S.fs[i] = fst[i];
+      __syncthreads();
+      // T1 = Fx^T Vxx', T2 = Fu^T Vxx', Qx, Qu
+      for (int e = tid; e < nx * nx; e += BW_BLOCK) {
+        const int i = e / nx, j = e % nx;
+        double acc = 0.0;
+        for (int k = 0; k < nx; ++k) acc += S.Fx[k * nx + i] * S.Vxx[k * nx + j];
+        S.T1[e] = acc;
+      }
+      for (int e = tid; e < NU * nx; e += BW_BLOCK) {
+        const int i = e / nx, j = e % nx;
+        double acc = 0.0;
+        for (int k = 0; k < nx; ++k) acc += S.Fu[k * NU + i] * S.Vxx[k * nx + j];
+        S.T2[e] = acc;
+      }
+      if (tid < nx) {
+        double acc = r[rec_off_Lx(nx) + tid];
+        for (int k = 0; k < nx; ++k) acc += S.Fx[k * nx + tid] * S.Vx[k];
+        S.Qx[tid] = acc;
+      } else if (tid >= 32 && tid < 32 + NU) {
+        const int i = tid - 32;
+        double acc = r[rec_off_Lu(nx) + i];
+        for (int k = 0; k < nx; ++k) acc += S.Fu[k * NU + i] * S.Vx[k];
+        S.Qu[i] = acc;
+      }
+      __syncthreads();
+      for (int e = tid; e < nx * nx; e += BW_BLOCK) {
+        const int i = e / nx, j = e % nx;
+        double acc = r[rec_off_Lxx(nx) + e];
+        for (int k = 0; k < nx; ++k) acc += S.T1[i * nx + k] * S.Fx[k * nx + j];
+        S.Qxx[e] = acc;
+      }
+      for (int e = tid; e < nx * NU; e += BW_BLOCK) {
+        const int i = e / NU, j = e % NU;
+        double acc = r[rec_off_Lxu(nx) + e];
+        for (int k = 0; k < nx; ++k) acc += S.T1[i * nx + k] * S.Fu[k * NU + j];
+        S.Qxu[e] = acc;
+      }
+      if (tid < NU * NU) {
+        const int i = tid / NU, j = tid % NU;
+        double acc = r[rec_off_Luu(nx) + tid];
+        for (int k = 0; k < nx; ++k) acc += S.T2[i * nx + k] * S.Fu[k * NU + j];
+        if (i == j) acc += preg;
+        S.Quu[tid] = acc;
+      }
+      __syncthreads();
+      // gains
+      if (tid == 0) {
+        bool ok = true;
+        if (!use_qp) {
+          for (int i = 0; i < NU; ++i)
+            for (int j = 0; j <= i; ++j) S.L[tri(i, j)] = S.Quu[i * NU + j];
+          ok = chol_packed<NU>(S.L);
+          for (int i = 0; i < NU; ++i) S.clamped[i] = 0;
+        } else {
+          double* kprev = d.k + ((long)b * N + t) * NU;
+          const double* ut = d.us + ((long)b * N + t) * NU;
+          double lb[NU], ub[NU], x[NU], q[NU];
+          for (int i = 0; i < NU; ++i) {
+            lb[i] = C.u_lb[i] - ut[i];
+            ub[i] = C.u_ub[i] - ut[i];
+            x[i] = kprev[i];
+            q[i] = S.Qu[i];
+          }
+          ok = boxqp(C, S.Quu, q, lb, ub, x, S.Qinv, S.clamped);
+          for (int i = 0; i < NU; ++i) S.kk[i] = -x[i];
+        }
+        S.flag = ok ? 0 : 1;
+      }
+      __syncthreads();
+      if (S.flag) {
+        failed = true;
+        break;
+      }
+      if (!use_qp) {
+        // K = Quu^-1 Qxu^T (one rhs per lane), k = Quu^-1 Qu
+        if (tid <= nx) {
+          double rhs[NU];
+          if (tid < nx)
+            for (int i = 0; i < NU; ++i) rhs[i] = S.Qxu[tid * NU + i];
+          else
+            for (int i = 0; i < NU; ++i) rhs[i] = S.Qu[i];
+          chol_solve<NU>(S.L, rhs);
+          if (tid < nx)
+            for (int i = 0; i < NU; ++i) S.K[i * nx + tid] = rhs[i];
+          else
+            for (int i = 0; i < NU; ++i) S.kk[i] = rhs[i];
+        }
+      } else {
+        for (int e = tid; e < NU * nx; e += BW_BLOCK) {
+          const int i = e / nx, j = e % nx;
+          double acc = 0.0;
+          for (int m = 0; m < NU; ++m) acc += S.Qinv[i * NU + m] * S.Qxu[j * NU + m];
+          S.K[e] = acc;
+        }
+      }
+      __syncthreads();
+      if (use_qp && tid == 0)
+        for (int i = 0; i < NU; ++i)
+          if (S.clamped[i]) S.Qu[i] = 0.0;
+      __syncthreads();
+      // Vx = Qx - K^T Qu ; Vxx = sym(Qxx - Qxu K) + preg I ; Vx += Vxx fs
+      for (int e = tid; e < nx * nx; e += BW_BLOCK) {
+        const int i = e / nx, j = e % nx;
+        double a1 = S.Qxx[i * nx + j], a2 = S.Qxx[j * nx + i];
+        for (int m = 0; m < NU; ++m) {
+          a1 -= S.Qxu[i * NU + m] * S.K[m * nx + j];
+          a2 -= S.Qxu[j * NU + m] * S.K[m * nx + i];
+        }
+        S.T1[e] = 0.5 * (a1 + a2) + (i == j ? preg : 0.0);  // new Vxx staged in T1
+      }
+      __syncthreads();
+      for (int e = tid; e < nx * nx; e += BW_BLOCK) S.Vxx[e] = S.T1[e];
+      __syncthreads();
+      double wt = 0.0;
+      if (tid < nx) {
+        double acc = S.Qx[tid];
+        for (int m = 0; m < NU; ++m) acc -= S.K[m * nx + tid] * S.Qu[m];
+        double vf = 0.0;
+        for (int j = 0; j < nx; ++j) vf += S.Vxx[tid * nx + j] * S.fs[j];
+        wt = vf;
+        if (!feas) acc += vf;
+        S.Vx[tid] = acc;
+      }
+      __syncthreads();
+      // NaN / inf checks, store gains and w_t = Vxx_t fs_t
+      {
+        bool badv = false;
+        for (int e = tid; e < nx * nx; e += BW_BLOCK) badv |= bad(fabs(S.Vxx[e]));
+        if (tid < nx) badv |= bad(fabs(S.Vx[tid]));
+        if (badv) S.flag = 1;
+      }
+      double* Kt = d.K + ((long)b * N + t) * NU * nx;
+      for (int e = tid; e < NU * nx; e += BW_BLOCK) Kt[e] = S.K[e];
+      if (tid < NU) d.k[((long)b * N + t) * NU + tid] = S.kk[tid];
+      if (tid < nx && !feas) d.w[((long)b * (N + 1) + t) * nx + tid] = wt;
+      __syncthreads();
+      if (S.flag) {
+        failed = true;
+        break;
+      }
+      if (tid == 0) {
+        // expected-improvement partials (SolverFDDP::updateExpectedImprovement)
+        double qk = 0.0, kqk = 0.0, qu2 = 0.0;
+        for (int i = 0; i < NU; ++i) {
+          double quk = 0.0;
+          for (int j = 0; j < NU; ++j) quk += S.Quu[i * NU + j] * S.kk[j];
+          qk += S.Qu[i] * S.kk[i];
+          kqk += S.kk[i] * quk;
+          qu2 += S.Qu[i] * S.Qu[i];
+        }
+        dg += qk;
+        dq -= kqk;
+        stop += qu2;
+        if (!feas) {
+          double a1 = 0.0, a2 = 0.0;
+          for (int i = 0; i < nx; ++i) {
+            double acc = 0.0;
+            for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
+            a1 += S.Vx[i] * S.fs[i];
+            a2 += S.fs[i] * acc;
+          }
+          dg -= a1;
+          dq += a2;
+        }
+      }
+    }
+    if (!failed) {
+      if (tid == 0) {
+        st->dg = dg;
+        st->dq = dq;
+        st->stop = stop;
+        st->preg = preg;
+        st->bw_ok = 1;
+        st->n_retries += retries;
+        st->n_backward += retries + 1;
+        st->n_iters += 1;
+      }
+      return;
+    }
+    // SolverFDDP::solve: increaseRegularization and retry without recalcDiff
+    retries++;
+    preg = fmin(preg * C.reg_inc, C.reg_max);
+    if (preg == C.reg_max) {
+      if (tid == 0) {
+        st->preg = preg;
+        st->bw_ok = 0;
+        st->iter = iter;
+        st->done = 1;
+        st->ok = 0;
+        st->n_retries += retries;
+        st->n_backward += retries;
+      }
+      return;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// line search: one lane per (instance, step length)
+// ---------------------------------------------------------------------------
+template <int NC, bool FF>
+__global__ __launch_bounds__(FW_BLOCK) void k_forward(const DevConsts* __restrict__ Cg, Dev d,
+                                                       const double* __restrict__ x0,
+                                                       const double* __restrict__ node_ref,
+                                                       const double* __restrict__ inst_ref,
+                                                       const uint8_t* __restrict__ surface) {
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  constexpr int nx = FF ? 21 : 14;
+  const long gid = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int b = (int)(gid / NTRIALS), tr = (int)(gid % NTRIALS);
+  if (b >= d.B) return;
+  const InstState* st = d.st + b;
+  if (st->done) return;
+  const double alpha = C.alphas[tr];
+  const bool feas = st->is_feasible != 0;
+  const bool gap = !(feas || alpha == 1.0);
+  const bool surf = surface[b] != 0;
+  const double* xreg = inst_ref + (long)b * 21;
+  const double* tauref = xreg + 14;
+  const double* yref = x0 + (long)b * nx;
+  double xh[21], xt[21], u[NU];
+  for (int i = 0; i < nx; ++i) xh[i] = x0[(long)b * nx + i];
+  double cost = 0.0, dv = 0.0;
+  bool fail = false;
+  double* xtr = d.xs_try + ((long)b * NTRIALS + tr) * (N + 1) * nx;
+  double* utr = d.us_try + ((long)b * NTRIALS + tr) * N * NU;
+  Primal P;
+  for (int t = 0; t <= N; ++t) {
+    const double* xs_t = d.xs + ((long)b * (N + 1) + t) * nx;
+    const double* fs_t = d.fs + ((long)b * (N + 1) + t) * nx;
+    for (int i = 0; i < nx; ++i) xt[i] = gap ? xh[i] + fs_t[i] * (alpha - 1.0) : xh[i];
+    if (!feas) {
+      const double* w_t = d.w + ((long)b * (N + 1) + t) * nx;
+      double acc = 0.0;
+      for (int i = 0; i < nx; ++i) acc += w_t[i] * (xs_t[i] - xt[i]);
+      dv -= acc;
+    }
+    for (int i = 0; i < nx; ++i) xtr[(long)t * nx + i] = xt[i];
+    const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
+    double c;
+    if (t < N) {
+      const double* us_t = d.us + ((long)b * N + t) * NU;
+      const double* K_t = d.K + ((long)b * N + t) * NU * nx;
+      const double* k_t = d.k + ((long)b * N + t) * NU;
+      for (int m = 0; m < NU; ++m) {
+        double acc = us_t[m] - k_t[m] * alpha;
+        for (int i = 0; i < nx; ++i) acc -= K_t[m * nx + i] * (xt[i] - xs_t[i]);
+        if (C.use_box) acc = fmin(fmax(acc, C.u_lb[m]), C.u_ub[m]);
+        u[m] = acc;
+        utr[(long)t * NU + m] = acc;
+      }
+      node_calc<NC, FF>(C, false, surf, xt, u, ref, xreg, tauref, yref, P, xh, c);
+      cost += c;
+      bool xbad = false;
+      for (int i = 0; i < nx; ++i) xbad |= bad(fabs(xh[i]));
+      if (bad(cost) || xbad) {
+        fail = true;
+        break;
+      }
+    } else {
+      double yn[21];
+      node_calc<NC, FF>(C, true, surf, xt, u, ref, xreg, tauref, yref, P, yn, c);
+      cost += c;
+      if (bad(cost)) fail = true;
+    }
+  }
+  d.trial[((long)b * NTRIALS + tr) * 2 + 0] = cost;
+  d.trial[((long)b * NTRIALS + tr) * 2 + 1] = dv;
+  d.trial_fail[(long)b * NTRIALS + tr] = fail ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// acceptance / regularisation / stopping: one lane per instance
+// ---------------------------------------------------------------------------
+__global__ void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter) {
+  const DevConsts& C = *Cg;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= d.B) return;
+  InstState s = d.st[b];
+  if (s.done) {
+    d.st[b].accepted = -1;
+    return;
+  }
+  s.iter = iter;
+  int acc = -1;
+  double steplength = C.alphas[NTRIALS - 1];
+  int tried = NTRIALS;
+  for (int tr = 0; tr < NTRIALS; ++tr) {
+    if (d.trial_fail[(long)b * NTRIALS + tr]) continue;
+    const double a = C.alphas[tr];
+    const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
+    const double dv = s.is_feasible ? 0.0 : d.trial[((long)b * NTRIALS + tr) * 2 + 1];
+    const double dV = s.cost - cost_try;
+    const double d0 = s.dg + dv, d1 = s.dq - 2.0 * dv;
+    const double dVexp = a * (d0 + 0.5 * a * d1);
+    bool ok;
+    if (dVexp >= 0)
+      ok = fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp;
+    else
+      ok = fabs(d0) < C.th_grad || dV < C.th_acceptnegstep * dVexp;
+    if (ok) {
+      acc = tr;
+      steplength = a;
+      tried = tr + 1;
+      s.was_feasible = s.is_feasible;
+      s.is_feasible = (s.was_feasible || a == 1.0) ? 1 : 0;
+      s.cost = cost_try;
+      s.recalc = 1;
+      break;
+    }
+  }
+  if (acc < 0) s.recalc = 0;  // (xs, us) unchanged: node data stays valid
+  s.n_trials += tried;
+  s.accepted = acc;
+  if (steplength > C.th_stepdec) s.preg = fmax(s.preg / C.reg_dec, C.reg_min);
+  if (steplength <= C.th_stepinc) {
+    s.preg = fmin(s.preg * C.reg_inc, C.reg_max);
+    if (s.preg == C.reg_max) {
+      s.done = 1;
+      s.ok = 0;
+    }
+  }
+  if (!s.done && s.was_feasible && s.stop < C.th_stop) {
+    s.done = 1;
+    s.ok = 1;
+  }
+  d.st[b] = s;
+}
+
+__global__ void k_commit(const DevConsts* __restrict__ Cg, Dev d) {
+  const DevConsts& C = *Cg;
+  const int N = C.N, nx = C.nx;
+  const long perX = (long)(N + 1) * nx, perU = (long)N * NU;
+  const long total = (long)d.B * (perX + perU);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / (perX + perU));
+    const long r = i % (perX + perU);
+    const int acc = d.st[b].accepted;
+    if (acc < 0) continue;
+    if (r < perX)
+      d.xs[(long)b * perX + r] = d.xs_try[((long)b * NTRIALS + acc) * perX + r];
+    else
+      d.us[(long)b * perU + (r - perX)] = d.us_try[((long)b * NTRIALS + acc) * perU + (r - perX)];
+  }
+}
+
+// solution read-back helpers: iter/ok, contact force at knots 0 and 1
+template <int NC, bool FF>
+__global__ __launch_bounds__(64) void k_finalize(const DevConsts* __restrict__ Cg, Dev d, int maxiter, const double* __restrict__ x0,
+                           const double* __restrict__ node_ref, const double* __restrict__ inst_ref,
+                           const uint8_t* __restrict__ surface, double* cost, int32_t* iters, uint8_t* ok,
+                           double* fn_pred, int32_t* stats) {
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  constexpr int nx = FF ? 21 : 14;
+  const long gid = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int b = (int)(gid / 2), knot = (int)(gid % 2);
+  if (b >= d.B) return;
+  const InstState s = d.st[b];
+  if (knot == 0) {
+    cost[b] = s.cost;
+    iters[b] = s.done ? s.iter : maxiter;
+    ok[b] = (s.done && s.ok) ? 1 : 0;
+    if (stats) {
+      stats[(long)b * 4 + 0] = s.n_iters;
+      stats[(long)b * 4 + 1] = s.n_trials;
+      stats[(long)b * 4 + 2] = s.n_retries;
+      stats[(long)b * 4 + 3] = s.n_backward;
+    }
+  }
+  if (fn_pred == nullptr) return;
+  const int t = knot < N ? knot : N - 1;
+  if (!surface[b]) {
+    fn_pred[(long)b * 2 + knot] = __builtin_nan("");
+    return;
+  }
+  const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
+  const double* u = d.us + ((long)b * N + t) * NU;
+  const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
+  const double* xreg = inst_ref + (long)b * 21;
+  Primal P;
+  double yn[21], c;
+  node_calc<NC, FF>(C, false, true, y, u, ref, xreg, xreg + 14, x0 + (long)b * nx, P, yn, c);
+  fn_pred[(long)b * 2 + knot] = (NC == 1) ? P.lam[0] : P.lam[2];
+}
+
+__global__ __launch_bounds__(64) void k_gravity(const ffddp_robot* __restrict__ rb, int B, const double* __restrict__ q,
+                          double* __restrict__ tau) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  gravity_torque(*rb, q + (long)b * NQ, tau + (long)b * NQ);
+}
+
+}  // namespace
+
+// ===========================================================================
+// host side
+// ===========================================================================
+struct ffddp_handle {
+  int device = 0;
+  int max_batch = 0;
+  DevConsts hc{};
+  DevConsts* dc = nullptr;
+  ffddp_robot* drb = nullptr;
+  Dev d{};
+  // staging for host-pointer API
+  double *in_x0 = nullptr, *in_nref = nullptr, *in_iref = nullptr, *in_xs = nullptr, *in_us = nullptr;
+  uint8_t* in_surf = nullptr;
+  double *out_xs = nullptr, *out_us = nullptr, *out_K = nullptr, *out_cost = nullptr, *out_fn = nullptr;
+  int32_t *out_iters = nullptr, *out_stats = nullptr;
+  uint8_t* out_ok = nullptr;
+  std::string err;
+};
+
+namespace {
+
+int fail(ffddp_handle* h, int code, const std::string& msg) {
+  if (h) h->err = msg;
+  return code;
+}
+
+#define HIPCHK(h, expr)                                                                    \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(h, FFDDP_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));  \
+  } while (0)
+
+void fill_consts(const ffddp_robot& rb, const ffddp_ocp_config& c, DevConsts& k) {
+  std::memset(&k, 0, sizeof(k));
+  k.rb = rb;
+  k.variant = c.variant;
+  k.N = c.horizon;
+  k.nc = c.nc;
+  k.use_box = c.use_box;
+  k.nx = c.variant == FFDDP_FORCE_FEEDBACK ? 21 : 14;
+  k.dt = c.dt;
+  k.inner_state_reg = c.variant == FFDDP_CLASSICAL ? 1 : c.use_inner_state_reg;
+  k.inner_tau_reg = c.variant == FFDDP_CLASSICAL ? 1 : c.use_inner_tau_reg;
+  k.w_post = c.w_posture;
+  k.w_v = c.w_v;
+  for (int i = 0; i < 7; ++i) k.vdw[i] = c.v_damp_weights[i];
+  // q soft limits (_make_q_soft_limit_cost, crocoddyl_classical.py:487-519)
+  k.has_qsoft = c.w_q_soft_limits > 0.0;
+  k.w_qs = c.w_q_soft_limits;
+  const double inf = __builtin_inf();
+  const double m = c.q_soft_limit_margin > 0.0 ? c.q_soft_limit_margin : 0.0;
+  for (int i = 0; i < 7; ++i) {
+    const double lo = c.q_lower[i], hi = c.q_upper[i];
+    const double qref = 0.5 * (lo + hi);
+    double lbs = lo + m, ubs = hi - m;
+    if (lbs > ubs) {
+      const double mid = 0.5 * (lo + hi);
+      lbs = mid - 1e-3;
+      ubs = mid + 1e-3;
+    }
+    k.qs_xref[i] = qref;
+    k.qs_lb[i] = lbs - qref;
+    k.qs_ub[i] = ubs - qref;
+    k.qs_xref[7 + i] = 0.0;
+    k.qs_lb[7 + i] = -inf;
+    k.qs_ub[7 + i] = inf;
+  }
+  k.w_ori = c.w_ee_ori;
+  for (int i = 0; i < 3; ++i) k.ori_w[i] = c.ori_weights[i];
+  k.w_wd = c.w_wdamp;
+  for (int i = 0; i < 3; ++i) k.wd_w[i] = c.w_wdamp_weights[i];
+  k.w_ee_pos = c.w_ee_pos;
+  k.ee_pos_w[0] = 1.0;
+  k.ee_pos_w[1] = 1.0;
+  k.ee_pos_w[2] = 2.5;
+  k.w_tp = c.w_tangent_pos;
+  k.w_tv = c.w_tangent_vel;
+  k.has_pz = c.w_plane_z > 0.0;
+  k.w_pz = c.w_plane_z;
+  k.has_vz = c.w_vz > 0.0;
+  k.w_vz = c.w_vz;
+  for (int i = 0; i < 9; ++i) k.Rdes[i] = c.R_des[i];
+  k.has_uni = c.w_unilateral > 0.0;
+  k.w_uni = c.w_unilateral;
+  if (c.nc == 1) {
+    k.uni_lb[0] = c.friction_margin;
+    k.uni_ub[0] = inf;
+  } else {
+    k.uni_lb[0] = k.uni_lb[1] = -inf;
+    k.uni_lb[2] = c.friction_margin;
+    k.uni_ub[0] = k.uni_ub[1] = k.uni_ub[2] = inf;
+  }
+  k.has_fn = c.w_fn > 0.0;
+  k.w_fn = c.w_fn;
+  if (c.nc == 1) {
+    k.fn_w[0] = 1.0;
+    k.fn_ref[0] = c.fn_des;
+  } else {
+    k.fn_w[0] = k.fn_w[1] = 0.0;
+    k.fn_w[2] = 1.0;
+    k.fn_ref[0] = k.fn_ref[1] = 0.0;
+    k.fn_ref[2] = c.fn_des;
+  }
+  k.w_tau = c.w_tau;
+  k.has_tsoft = c.w_tau_soft_limits > 0.0;
+  k.w_ts = c.w_tau_soft_limits;
+  double mn = c.tau_limits[0];
+  for (int i = 1; i < 7; ++i) mn = c.tau_limits[i] < mn ? c.tau_limits[i] : mn;
+  double mg = c.tau_soft_limit_margin > 0.0 ? c.tau_soft_limit_margin : 0.0;
+  mg = mg < mn - 1.0e-6 ? mg : mn - 1.0e-6;
+  for (int i = 0; i < 7; ++i) {
+    k.ts_lb[i] = -c.tau_limits[i] + mg;
+    k.ts_ub[i] = c.tau_limits[i] - mg;
+    k.u_lb[i] = -c.tau_limits[i];
+    k.u_ub[i] = c.tau_limits[i];
+  }
+  k.Kp = c.contact_gains[0];
+  k.Kd = c.contact_gains[1];
+  k.eps = c.contact_inv_damping;
+  k.z_press = c.z_press;
+  // force feedback (_AugmentedLPFActionModel.__init__, :170-188)
+  double al = c.ff_alpha;
+  al = al < 0.0 ? 0.0 : (al > 0.999999 ? 0.999999 : al);
+  k.alpha = al;
+  k.beta = 1.0 - al;
+  k.w_w = c.w_w > 0.0 ? c.w_w : 0.0;
+  k.w_ws = c.w_w_soft_limits > 0.0 ? c.w_w_soft_limits : 0.0;
+  const double wm = c.tau_soft_limit_margin > 0.0 ? c.tau_soft_limit_margin : 0.0;
+  for (int i = 0; i < 7; ++i) {
+    const double l = c.tau_limits[i] - wm;
+    k.ws_lim[i] = l > 1.0e-9 ? l : 1.0e-9;
+  }
+  k.w_y = c.w_y > 0.0 ? c.w_y : 0.0;
+  for (int i = 0; i < 21; ++i) k.Wy2[i] = c.y_weights[i] * c.y_weights[i];
+  // solver constants (SolverBoxFDDP / SolverFDDP / BoxQP defaults)
+  k.th_stop = c.use_box ? 5e-5 : 1e-9;
+  k.th_grad = 1e-12;
+  k.th_acceptstep = 0.1;
+  k.th_acceptnegstep = 2.0;
+  k.th_stepdec = 0.5;
+  k.th_stepinc = 0.01;
+  k.reg_min = 1e-9;
+  k.reg_max = 1e9;
+  k.reg_inc = 10.0;
+  k.reg_dec = 10.0;
+  for (int i = 0; i < NTRIALS; ++i) k.alphas[i] = 1.0 / (double)(1 << i);
+  k.qp_maxiter = 100;
+  k.qp_th_acceptstep = 0.1;
+  k.qp_th_grad = 1e-5;
+  k.qp_reg = 0.0;
+}
+
+template <class T> int dalloc(ffddp_handle* h, T** p, size_t n) {
+  if (hipMalloc((void**)p, n * sizeof(T) + 64) != hipSuccess) {
+    *p = nullptr;
+    return fail(h, FFDDP_E_OOM, "hipMalloc failed");
+  }
+  return 0;
+}
+
+void free_all(ffddp_handle* h) {
+  void* ps[] = {h->dc, h->drb, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
+                h->d.us_try, h->d.trial, h->d.trial_fail, h->d.st, h->in_x0, h->in_nref, h->in_iref, h->in_xs,
+                h->in_us, h->in_surf, h->out_xs, h->out_us, h->out_K, h->out_cost, h->out_fn, h->out_iters,
+                h->out_stats, h->out_ok};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+}
+
+template <int NC, bool FF>
+int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref, const double* iref,
+                 const uint8_t* surf, const double* xs_init, const double* us_init, int maxiter, int is_feasible,
+                 double* xs, double* us, double* K, double* cost, int32_t* iters, uint8_t* ok, double* fn_pred,
+                 int32_t* stats, hipStream_t s) {
+  Dev d = h->d;
+  d.B = B;
+  const int N = h->hc.N, nx = h->hc.nx;
+  hipLaunchKernelGGL(k_init, dim3(1024), dim3(256), 0, s, h->dc, d, xs_init, us_init, is_feasible);
+  const long nodes = (long)B * (N + 1);
+  const int node_blocks = (int)((nodes + NODE_GPB - 1) / NODE_GPB);
+  const int fw_blocks = (int)(((long)B * NTRIALS + FW_BLOCK - 1) / FW_BLOCK);
+  for (int it = 0; it < maxiter; ++it) {
+    hipLaunchKernelGGL((k_node<NC, FF>), dim3(node_blocks), dim3(NODE_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf, 0);
+    hipLaunchKernelGGL((k_backward<FF>), dim3(B), dim3(BW_BLOCK), 0, s, h->dc, d, it);
+    hipLaunchKernelGGL((k_forward<NC, FF>), dim3(fw_blocks), dim3(FW_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf);
+    hipLaunchKernelGGL(k_accept, dim3((B + 255) / 256), dim3(256), 0, s, h->dc, d, it);
+    hipLaunchKernelGGL(k_commit, dim3(2048), dim3(256), 0, s, h->dc, d);
+  }
+  hipLaunchKernelGGL((k_finalize<NC, FF>), dim3((2 * B + 63) / 64), dim3(64), 0, s, h->dc, d, maxiter, x0, nref, iref,
+                     surf, cost, iters, ok, fn_pred, stats);
+  if (hipGetLastError() != hipSuccess) return fail(h, FFDDP_E_DEVICE, "kernel launch failed");
+  const size_t bx = (size_t)B * (N + 1) * nx * sizeof(double);
+  const size_t bu = (size_t)B * N * NU * sizeof(double);
+  const size_t bk = (size_t)B * N * NU * nx * sizeof(double);
+  HIPCHK(h, hipMemcpyAsync(xs, d.xs, bx, hipMemcpyDeviceToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(us, d.us, bu, hipMemcpyDeviceToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(K, d.K, bk, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+int launch_solve(ffddp_handle* h, int B, const double* x0, const double* nref, const double* iref,
+                 const uint8_t* surf, const double* xs_init, const double* us_init, int maxiter, int is_feasible,
+                 double* xs, double* us, double* K, double* cost, int32_t* iters, uint8_t* ok, double* fn_pred,
+                 int32_t* stats, hipStream_t s) {
+  const bool ff = h->hc.variant == FFDDP_FORCE_FEEDBACK;
+  const int nc = h->hc.nc;
+#define FFDDP_LS(NC_, FF_) \
+  launch_solve_t<NC_, FF_>(h, B, x0, nref, iref, surf, xs_init, us_init, maxiter, is_feasible, xs, us, K, cost, iters, ok, fn_pred, stats, s)
+  if (nc == 1) return ff ? FFDDP_LS(1, true) : FFDDP_LS(1, false);
+  return ff ? FFDDP_LS(3, true) : FFDDP_LS(3, false);
+#undef FFDDP_LS
+}
+
+template <int NC, bool FF>
+void launch_node(ffddp_handle* h, Dev d, int B, hipStream_t s, int force_all) {
+  const long nodes = (long)B * (h->hc.N + 1);
+  hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, s, h->dc,
+                     d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all);
+}
+
+bool valid_cfg(const ffddp_ocp_config& c) {
+  return (c.variant == FFDDP_CLASSICAL || c.variant == FFDDP_FORCE_FEEDBACK) && c.horizon >= 1 &&
+         c.horizon <= 4096 && (c.nc == 1 || c.nc == 3) && c.dt > 0.0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int device, int max_batch,
+                 ffddp_handle** out) {
+  if (!robot || !cfg || !out || max_batch < 1) return FFDDP_E_INVALID;
+  *out = nullptr;
+  if (!valid_cfg(*cfg)) return FFDDP_E_INVALID;
+  ffddp_handle* h = new (std::nothrow) ffddp_handle();
+  if (!h) return FFDDP_E_OOM;
+  h->device = device;
+  h->max_batch = max_batch;
+  fill_consts(*robot, *cfg, h->hc);
+  if (hipSetDevice(device) != hipSuccess) {
+    delete h;
+    return FFDDP_E_DEVICE;
+  }
+  const long B = max_batch, N = cfg->horizon, nx = h->hc.nx;
+  Dev& d = h->d;
+  d.N = (int)N;
+  d.nx = (int)nx;
+  d.rec = rec_size((int)nx);
+  int rc = 0;
+  rc |= dalloc(h, &h->dc, 1);
+  rc |= dalloc(h, &h->drb, 1);
+  rc |= dalloc(h, &d.rec_buf, (size_t)B * (N + 1) * d.rec);
+  rc |= dalloc(h, &d.fs, (size_t)B * (N + 1) * nx);
+  rc |= dalloc(h, &d.xs, (size_t)B * (N + 1) * nx);
+  rc |= dalloc(h, &d.us, (size_t)B * N * NU);
+  rc |= dalloc(h, &d.K, (size_t)B * N * NU * nx);
+  rc |= dalloc(h, &d.k, (size_t)B * N * NU);
+  rc |= dalloc(h, &d.w, (size_t)B * (N + 1) * nx);
+  rc |= dalloc(h, &d.xs_try, (size_t)B * NTRIALS * (N + 1) * nx);
+  rc |= dalloc(h, &d.us_try, (size_t)B * NTRIALS * N * NU);
+  rc |= dalloc(h, &d.trial, (size_t)B * NTRIALS * 2);
+  rc |= dalloc(h, &d.trial_fail, (size_t)B * NTRIALS);
+  rc |= dalloc(h, &d.st, (size_t)B);
+  rc |= dalloc(h, &h->in_x0, (size_t)B * nx);
+  rc |= dalloc(h, &h->in_nref, (size_t)B * (N + 1) * 6);
+  rc |= dalloc(h, &h->in_iref, (size_t)B * 21);
+  rc |= dalloc(h, &h->in_xs, (size_t)B * (N + 1) * nx);
+  rc |= dalloc(h, &h->in_us, (size_t)B * N * NU);
+  rc |= dalloc(h, &h->in_surf, (size_t)B);
+  rc |= dalloc(h, &h->out_xs, (size_t)B * (N + 1) * nx);
+  rc |= dalloc(h, &h->out_us, (size_t)B * N * NU);
+  rc |= dalloc(h, &h->out_K, (size_t)B * N * NU * nx);
+  rc |= dalloc(h, &h->out_cost, (size_t)B);
+  rc |= dalloc(h, &h->out_fn, (size_t)B * 2);
+  rc |= dalloc(h, &h->out_iters, (size_t)B);
+  rc |= dalloc(h, &h->out_stats, (size_t)B * 4);
+  rc |= dalloc(h, &h->out_ok, (size_t)B);
+  if (rc) {
+    free_all(h);
+    delete h;
+    return FFDDP_E_OOM;
+  }
+  if (hipMemcpy(h->dc, &h->hc, sizeof(DevConsts), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->drb, robot, sizeof(ffddp_robot), hipMemcpyHostToDevice) != hipSuccess) {
+    free_all(h);
+    delete h;
+    return FFDDP_E_DEVICE;
+  }
+  *out = h;
+  return 0;
+}
+
+void ffddp_destroy(ffddp_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  free_all(h);
+  delete h;
+}
+
+const char* ffddp_last_error(const ffddp_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double* node_ref, const double* inst_ref,
+                          const uint8_t* surface, const double* xs_init, const double* us_init, int maxiter,
+                          int is_feasible, double* xs, double* us, double* K, double* cost, int32_t* iters,
+                          uint8_t* ok, double* fn_pred, int32_t* stats, void* stream) {
+  if (!h) return FFDDP_E_INVALID;
+  if (B < 0 || maxiter < 0) return fail(h, FFDDP_E_INVALID, "negative B or maxiter");
+  if (B > h->max_batch) return fail(h, FFDDP_E_CAPACITY, "B exceeds max_batch");
+  if (B == 0) return 0;
+  if (!x0 || !node_ref || !inst_ref || !surface || !xs_init || !us_init || !xs || !us || !K || !cost || !iters || !ok)
+    return fail(h, FFDDP_E_INVALID, "null pointer");
+  HIPCHK(h, hipSetDevice(h->device));
+  return launch_solve(h, B, x0, node_ref, inst_ref, surface, xs_init, us_init, maxiter, is_feasible, xs, us, K,
+                      cost, iters, ok, fn_pred, stats, (hipStream_t)stream);
+}
+
+int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* node_ref, const double* inst_ref,
+                      const uint8_t* surface, const double* xs_init, const double* us_init, int maxiter,
+                      int is_feasible, double* xs, double* us, double* K, double* cost, int32_t* iters, uint8_t* ok,
+                      double* fn_pred, int32_t* stats) {
+  if (!h) return FFDDP_E_INVALID;
+  if (B < 0 || maxiter < 0) return fail(h, FFDDP_E_INVALID, "negative B or maxiter");
+  if (B > h->max_batch) return fail(h, FFDDP_E_CAPACITY, "B exceeds max_batch");
+  if (B == 0) return 0;
+  if (!x0 || !node_ref || !inst_ref || !surface || !xs_init || !us_init || !xs || !us || !K || !cost || !iters || !ok)
+    return fail(h, FFDDP_E_INVALID, "null pointer");
+  HIPCHK(h, hipSetDevice(h->device));
+  const long N = h->hc.N, nx = h->hc.nx;
+  const size_t bx = (size_t)B * (N + 1) * nx * 8, bu = (size_t)B * N * NU * 8, bk = (size_t)B * N * NU * nx * 8;
+  HIPCHK(h, hipMemcpy(h->in_x0, x0, (size_t)B * nx * 8, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_nref, node_ref, (size_t)B * (N + 1) * 6 * 8, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_iref, inst_ref, (size_t)B * 21 * 8, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_surf, surface, (size_t)B, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_xs, xs_init, bx, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_us, us_init, bu, hipMemcpyHostToDevice));
+  int rc = launch_solve(h, B, h->in_x0, h->in_nref, h->in_iref, h->in_surf, h->in_xs, h->in_us, maxiter, is_feasible,
+                        h->out_xs, h->out_us, h->out_K, h->out_cost, h->out_iters, h->out_ok, h->out_fn,
+                        h->out_stats, nullptr);
+  if (rc) return rc;
+  HIPCHK(h, hipDeviceSynchronize());
+  HIPCHK(h, hipMemcpy(xs, h->out_xs, bx, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(us, h->out_us, bu, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(K, h->out_K, bk, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(cost, h->out_cost, (size_t)B * 8, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(iters, h->out_iters, (size_t)B * 4, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(ok, h->out_ok, (size_t)B, hipMemcpyDeviceToHost));
+  if (fn_pred) HIPCHK(h, hipMemcpy(fn_pred, h->out_fn, (size_t)B * 2 * 8, hipMemcpyDeviceToHost));
+  if (stats) HIPCHK(h, hipMemcpy(stats, h->out_stats, (size_t)B * 4 * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ffddp_calc_diff(ffddp_handle* h, int B, const double* x0, const double* node_ref, const double* inst_ref,
+                    const uint8_t* surface, const double* xs, const double* us, double* Fx, double* Fu, double* Lx,
+                    double* Lu, double* Lxx, double* Lxu, double* Luu, double* cost, double* xnext, double* lam) {
+  if (!h) return FFDDP_E_INVALID;
+  if (B < 1 || B > h->max_batch) return fail(h, FFDDP_E_CAPACITY, "bad B");
+  HIPCHK(h, hipSetDevice(h->device));
+  const int N = h->hc.N, nx = h->hc.nx, R = h->d.rec;
+  const bool ff = h->hc.variant == FFDDP_FORCE_FEEDBACK;
+  Dev d = h->d;
+  d.B = B;
+  HIPCHK(h, hipMemcpy(h->in_x0, x0, (size_t)B * nx * 8, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_nref, node_ref, (size_t)B * (N + 1) * 6 * 8, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_iref, inst_ref, (size_t)B * 21 * 8, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_surf, surface, (size_t)B, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_xs, xs, (size_t)B * (N + 1) * nx * 8, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->in_us, us, (size_t)B * N * NU * 8, hipMemcpyHostToDevice));
+  // node kernel reads (xs, us) from the solver state: initialise it from the inputs
+  hipLaunchKernelGGL(k_init, dim3(1024), dim3(256), 0, nullptr, h->dc, d, h->in_xs, h->in_us, 0);
+  if (h->hc.nc == 1)
+    ff ? launch_node<1, true>(h, d, B, nullptr, 1) : launch_node<1, false>(h, d, B, nullptr, 1);
+  else
+    ff ? launch_node<3, true>(h, d, B, nullptr, 1) : launch_node<3, false>(h, d, B, nullptr, 1);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipDeviceSynchronize());
+  std::vector<double> rec((size_t)B * (N + 1) * R), fsv((size_t)B * (N + 1) * nx);
+  HIPCHK(h, hipMemcpy(rec.data(), d.rec_buf, rec.size() * 8, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(fsv.data(), d.fs, fsv.size() * 8, hipMemcpyDeviceToHost));
+  const double dt = h->hc.dt;
+  for (int b = 0; b < B; ++b) {
+    for (int t = 0; t <= N; ++t) {
+      const double* r = rec.data() + ((size_t)b * (N + 1) + t) * R;
+      const size_t nt = (size_t)b * (N + 1) + t;
+      for (int i = 0; i < nx; ++i) Lx[nt * nx + i] = r[rec_off_Lx(nx) + i];
+      for (int e = 0; e < nx * nx; ++e) Lxx[nt * nx * nx + e] = r[rec_off_Lxx(nx) + e];
+      cost[nt] = r[rec_off_cost(nx)];
+      for (int c = 0; c < 3; ++c) lam[nt * 3 + c] = r[rec_off_lam(nx) + c];
+      if (t == N) continue;
+      const size_t rt = (size_t)b * N + t;
+      const double* A = r + rec_off_A();
+      for (int i = 0; i < NU; ++i) Lu[rt * NU + i] = r[rec_off_Lu(nx) + i];
+      for (int e = 0; e < nx * NU; ++e) Lxu[rt * nx * NU + e] = r[rec_off_Lxu(nx) + e];
+      for (int e = 0; e < NU * NU; ++e) Luu[rt * NU * NU + e] = r[rec_off_Luu(nx) + e];
+      for (int i = 0; i < nx; ++i) {
+        for (int j = 0; j < nx; ++j) {
+          double v = (i == j) ? 1.0 : 0.0;
+          if (i < 14 && j < (ff ? 21 : 14)) {
+            v += (i < 7 ? dt * dt : dt) * A[j * NQ + (i % 7)];
+            if (i < 7 && j == i + 7) v += dt;
+          }
+          if (ff && i >= 14) v = (i == j) ? h->hc.alpha : 0.0;
+          Fx[rt * nx * nx + i * nx + j] = v;
+        }
+        for (int kk = 0; kk < NU; ++kk) {
+          double v;
+          if (!ff)
+            v = (i < 7 ? dt * dt : dt) * A[(14 + kk) * NQ + (i % 7)];
+          else
+            v = (i >= 14 && i - 14 == kk) ? h->hc.beta : 0.0;
+          Fu[rt * nx * NU + i * NU + kk] = v;
+        }
+      }
+      // xnext = xs[t+1] + fs[t+1]  (fs computed with is_feasible = 0)
+      for (int i = 0; i < nx; ++i)
+        xnext[rt * nx + i] = xs[((size_t)b * (N + 1) + t + 1) * nx + i] + fsv[((size_t)b * (N + 1) + t + 1) * nx + i];
+    }
+  }
+  return 0;
+}
+
+int ffddp_frame_placement(const ffddp_robot* robot, const double* q, double* R, double* p) {
+  if (!robot || !q || !R || !p) return FFDDP_E_INVALID;
+  RBOut<double> o;
+  const double zero[NQ] = {0, 0, 0, 0, 0, 0, 0};
+  rb_pass<double, false, false>(*robot, q, zero, zero, nullptr, o, nullptr);
+  for (int i = 0; i < 9; ++i) R[i] = o.Ree.m[i];
+  p[0] = o.pee.x;
+  p[1] = o.pee.y;
+  p[2] = o.pee.z;
+  return 0;
+}
+
+int ffddp_gravity_torque(const ffddp_robot* robot, int B, const double* q, double* tau) {
+  if (!robot || !q || !tau || B < 0) return FFDDP_E_INVALID;
+  for (int b = 0; b < B; ++b) gravity_torque(*robot, q + (size_t)b * NQ, tau + (size_t)b * NQ);
+  return 0;
+}
+
+int ffddp_gravity_torque_dev(ffddp_handle* h, int B, const double* q, double* tau, void* stream) {
+  if (!h || B < 0) return FFDDP_E_INVALID;
+  if (B == 0) return 0;
+  HIPCHK(h, hipSetDevice(h->device));
+  hipLaunchKernelGGL(k_gravity, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, h->drb, B, q, tau);
+  HIPCHK(h, hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

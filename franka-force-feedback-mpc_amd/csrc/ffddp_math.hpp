@@ -1,0 +1,152 @@
+// ffddp_math.hpp — fixed-size fp64 algebra for the 7-DoF arm, generic over a
+// scalar T in {double, Dual}.  Dual carries ONE forward-mode tangent: in the
+// calcDiff kernel every lane of a 16-lane node group propagates a different
+// state direction through the same primal code, so each lane produces one
+// column of the analytic Jacobians (Pinocchio's computeRNEADerivatives /
+// getFrame{Velocity,Acceleration}Derivatives, which the reference reaches via
+// Crocoddyl, crocoddyl_classical.py:619, 722).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#define FFD_HD __host__ __device__ __forceinline__
+
+namespace ffddp {
+
+struct Dual {
+  double v, d;
+};
+
+FFD_HD Dual operator+(Dual a, Dual b) { return {a.v + b.v, a.d + b.d}; }
+FFD_HD Dual operator-(Dual a, Dual b) { return {a.v - b.v, a.d - b.d}; }
+FFD_HD Dual operator-(Dual a) { return {-a.v, -a.d}; }
+FFD_HD Dual operator*(Dual a, Dual b) { return {a.v * b.v, a.v * b.d + a.d * b.v}; }
+FFD_HD Dual operator*(double s, Dual a) { return {s * a.v, s * a.d}; }
+FFD_HD Dual operator*(Dual a, double s) { return {s * a.v, s * a.d}; }
+FFD_HD Dual operator+(Dual a, double s) { return {a.v + s, a.d}; }
+FFD_HD Dual operator+(double s, Dual a) { return {a.v + s, a.d}; }
+FFD_HD Dual operator-(Dual a, double s) { return {a.v - s, a.d}; }
+FFD_HD Dual operator-(double s, Dual a) { return {s - a.v, -a.d}; }
+FFD_HD Dual& operator+=(Dual& a, Dual b) { a.v += b.v; a.d += b.d; return a; }
+FFD_HD Dual& operator-=(Dual& a, Dual b) { a.v -= b.v; a.d -= b.d; return a; }
+
+FFD_HD double val(double x) { return x; }
+FFD_HD double val(Dual x) { return x.v; }
+FFD_HD double tng(double) { return 0.0; }
+FFD_HD double tng(Dual x) { return x.d; }
+
+template <class T> FFD_HD T mk(double v, double d);
+template <> FFD_HD double mk<double>(double v, double) { return v; }
+template <> FFD_HD Dual mk<Dual>(double v, double d) { return {v, d}; }
+
+FFD_HD void sincos_(double q, double& s, double& c) {
+#ifdef __HIP_DEVICE_COMPILE__
+  sincos(q, &s, &c);
+#else
+  s = sin(q);
+  c = cos(q);
+#endif
+}
+FFD_HD void sincos_(Dual q, Dual& s, Dual& c) {
+  double sv, cv;
+  sincos_(q.v, sv, cv);
+  s = {sv, q.d * cv};
+  c = {cv, -q.d * sv};
+}
+
+template <class T> struct V3 {
+  T x, y, z;
+};
+
+template <class T> FFD_HD V3<T> operator+(V3<T> a, V3<T> b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+template <class T> FFD_HD V3<T> operator-(V3<T> a, V3<T> b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+template <class T> FFD_HD V3<T> operator*(T s, V3<T> a) { return {s * a.x, s * a.y, s * a.z}; }
+template <class T> FFD_HD V3<T> scale(V3<T> a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+template <class T> FFD_HD V3<T> cross(V3<T> a, V3<T> b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+template <class T> FFD_HD T dot(V3<T> a, V3<T> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+template <class T> FFD_HD V3<T> v3zero() { return {T{}, T{}, T{}}; }
+template <class T> FFD_HD V3<T> v3c(const double* p) {
+  return {mk<T>(p[0], 0.0), mk<T>(p[1], 0.0), mk<T>(p[2], 0.0)};
+}
+
+// 3x3, row-major
+template <class T> struct M3 {
+  T m[9];
+};
+template <class T> FFD_HD M3<T> m3eye() {
+  M3<T> r;
+  for (int i = 0; i < 9; ++i) r.m[i] = mk<T>((i % 4 == 0) ? 1.0 : 0.0, 0.0);
+  return r;
+}
+template <class T> FFD_HD V3<T> mul(const M3<T>& A, V3<T> x) {
+  return {A.m[0] * x.x + A.m[1] * x.y + A.m[2] * x.z, A.m[3] * x.x + A.m[4] * x.y + A.m[5] * x.z,
+          A.m[6] * x.x + A.m[7] * x.y + A.m[8] * x.z};
+}
+template <class T> FFD_HD V3<T> mulT(const M3<T>& A, V3<T> x) {
+  return {A.m[0] * x.x + A.m[3] * x.y + A.m[6] * x.z, A.m[1] * x.x + A.m[4] * x.y + A.m[7] * x.z,
+          A.m[2] * x.x + A.m[5] * x.y + A.m[8] * x.z};
+}
+// A (T) * B (double constant)
+template <class T> FFD_HD M3<T> mulc(const M3<T>& A, const double* B) {
+  M3<T> r;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      r.m[3 * i + j] = A.m[3 * i + 0] * B[0 * 3 + j] + A.m[3 * i + 1] * B[1 * 3 + j] + A.m[3 * i + 2] * B[2 * 3 + j];
+  return r;
+}
+template <class T> FFD_HD V3<T> mulc_v(const M3<T>& A, const double* p) {
+  return {A.m[0] * p[0] + A.m[1] * p[1] + A.m[2] * p[2], A.m[3] * p[0] + A.m[4] * p[1] + A.m[5] * p[2],
+          A.m[6] * p[0] + A.m[7] * p[1] + A.m[8] * p[2]};
+}
+// constant symmetric 3x3 (row-major, double) times vector
+template <class T> FFD_HD V3<T> cmul(const double* I, V3<T> x) {
+  return {I[0] * x.x + I[1] * x.y + I[2] * x.z, I[3] * x.x + I[4] * x.y + I[5] * x.z,
+          I[6] * x.x + I[7] * x.y + I[8] * x.z};
+}
+
+// ---------------------------------------------------------------------------
+// packed lower-triangular Cholesky (Eigen::LLT semantics: fail if pivot <= 0)
+// ---------------------------------------------------------------------------
+FFD_HD int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+
+template <int N> FFD_HD bool chol_packed(double* A /* packed lower, in-place */) {
+  for (int j = 0; j < N; ++j) {
+    double d = A[tri(j, j)];
+    for (int k = 0; k < j; ++k) d -= A[tri(j, k)] * A[tri(j, k)];
+    if (!(d > 0.0)) return false;
+    const double l = sqrt(d);
+    A[tri(j, j)] = l;
+    const double il = 1.0 / l;
+    for (int i = j + 1; i < N; ++i) {
+      double s = A[tri(i, j)];
+      for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
+      A[tri(i, j)] = s * il;
+    }
+  }
+  return true;
+}
+// solve L y = b in place
+template <int N> FFD_HD void fwd_sub(const double* L, double* b) {
+  for (int i = 0; i < N; ++i) {
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= L[tri(i, k)] * b[k];
+    b[i] = s / L[tri(i, i)];
+  }
+}
+// solve L^T x = y in place
+template <int N> FFD_HD void bwd_sub(const double* L, double* b) {
+  for (int i = N - 1; i >= 0; --i) {
+    double s = b[i];
+    for (int k = i + 1; k < N; ++k) s -= L[tri(k, i)] * b[k];
+    b[i] = s / L[tri(i, i)];
+  }
+}
+template <int N> FFD_HD void chol_solve(const double* L, double* b) {
+  fwd_sub<N>(L, b);
+  bwd_sub<N>(L, b);
+}
+
+}  // namespace ffddp

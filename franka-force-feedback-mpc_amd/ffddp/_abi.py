@@ -1,0 +1,206 @@
+"""ctypes binding of include/ffddp.h (the drop-in C-ABI).
+
+The library is built in-tree (franka-force-feedback-mpc_amd/lib/libffddp.so)
+by __graft_entry__.build() / `make -C franka-force-feedback-mpc_amd/csrc`.
+There is no CPU fallback: if the library is missing, import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import robot as R
+
+LIB_PATH = Path(__file__).resolve().parents[1] / "lib" / "libffddp.so"
+
+FFDDP_CLASSICAL = 0
+FFDDP_FORCE_FEEDBACK = 1
+
+SYMBOLS = (
+    "ffddp_create",
+    "ffddp_destroy",
+    "ffddp_last_error",
+    "ffddp_solve_batch",
+    "ffddp_solve_batch_dev",
+    "ffddp_calc_diff",
+    "ffddp_frame_placement",
+    "ffddp_gravity_torque",
+    "ffddp_gravity_torque_dev",
+)
+
+
+class Robot(C.Structure):
+    _fields_ = [
+        ("joint_R", C.c_double * 9 * 7),
+        ("joint_p", C.c_double * 3 * 7),
+        ("mass", C.c_double * 7),
+        ("com", C.c_double * 3 * 7),
+        ("inertia", C.c_double * 9 * 7),
+        ("ee_R", C.c_double * 9),
+        ("ee_p", C.c_double * 3),
+        ("gravity", C.c_double * 3),
+    ]
+
+
+class OcpConfig(C.Structure):
+    _fields_ = [
+        ("variant", C.c_int32),
+        ("horizon", C.c_int32),
+        ("nc", C.c_int32),
+        ("use_box", C.c_int32),
+        ("dt", C.c_double),
+        ("z_press", C.c_double),
+        ("w_ee_pos", C.c_double),
+        ("w_ee_ori", C.c_double),
+        ("ori_weights", C.c_double * 3),
+        ("w_posture", C.c_double),
+        ("w_v", C.c_double),
+        ("v_damp_weights", C.c_double * 7),
+        ("w_tau", C.c_double),
+        ("w_tau_soft_limits", C.c_double),
+        ("tau_soft_limit_margin", C.c_double),
+        ("w_q_soft_limits", C.c_double),
+        ("q_soft_limit_margin", C.c_double),
+        ("q_lower", C.c_double * 7),
+        ("q_upper", C.c_double * 7),
+        ("w_tangent_pos", C.c_double),
+        ("w_tangent_vel", C.c_double),
+        ("w_plane_z", C.c_double),
+        ("w_vz", C.c_double),
+        ("w_unilateral", C.c_double),
+        ("friction_margin", C.c_double),
+        ("w_fn", C.c_double),
+        ("fn_des", C.c_double),
+        ("w_wdamp", C.c_double),
+        ("w_wdamp_weights", C.c_double * 3),
+        ("contact_gains", C.c_double * 2),
+        ("contact_inv_damping", C.c_double),
+        ("tau_limits", C.c_double * 7),
+        ("R_des", C.c_double * 9),
+        ("ff_alpha", C.c_double),
+        ("w_w", C.c_double),
+        ("w_w_soft_limits", C.c_double),
+        ("w_y", C.c_double),
+        ("y_weights", C.c_double * 21),
+        ("use_inner_state_reg", C.c_int32),
+        ("use_inner_tau_reg", C.c_int32),
+    ]
+
+
+def _fill(arr, values):
+    flat = np.asarray(values, dtype=float).reshape(-1)
+    buf = (C.c_double * flat.size).from_buffer(arr)
+    for i, v in enumerate(flat):
+        buf[i] = float(v)
+
+
+def make_robot() -> Robot:
+    rb = Robot()
+    _fill(rb.joint_R, R.JOINT_R)
+    _fill(rb.joint_p, R.JOINT_P)
+    _fill(rb.mass, R.MASS)
+    _fill(rb.com, R.COM)
+    _fill(rb.inertia, R.INERTIA)
+    _fill(rb.ee_R, R.EE_R)
+    _fill(rb.ee_p, R.EE_P)
+    _fill(rb.gravity, R.GRAVITY)
+    return rb
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libffddp.so.  Raises (never falls back) when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # One HIP runtime per process: torch wheels ship their own libamdhip64.so.7
+    # and load it by path; if ours (/opt/rocm) were loaded first, torch would
+    # bring a second runtime and fail to initialise.  Importing torch first makes
+    # the dynamic loader bind our NEEDED libamdhip64.so.7 to the torch copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    path = Path(os.environ.get("FFDDP_LIB", str(LIB_PATH)))
+    if not path.exists():
+        raise ImportError(
+            f"ffddp: HIP library not found at {path}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)"
+        )
+    lib = C.CDLL(str(path))
+    dp, ip, up, vp = C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_uint8), C.c_void_p
+    lib.ffddp_create.argtypes = [C.POINTER(Robot), C.POINTER(OcpConfig), C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    lib.ffddp_create.restype = C.c_int
+    lib.ffddp_destroy.argtypes = [C.c_void_p]
+    lib.ffddp_destroy.restype = None
+    lib.ffddp_last_error.argtypes = [C.c_void_p]
+    lib.ffddp_last_error.restype = C.c_char_p
+    solve_args = [C.c_void_p, C.c_int, dp, dp, dp, up, dp, dp, C.c_int, C.c_int, dp, dp, dp, dp, ip, up, dp, ip]
+    lib.ffddp_solve_batch.argtypes = solve_args
+    lib.ffddp_solve_batch.restype = C.c_int
+    dev_args = [C.c_void_p, C.c_int] + [vp] * 6 + [C.c_int, C.c_int] + [vp] * 8 + [vp]
+    lib.ffddp_solve_batch_dev.argtypes = dev_args
+    lib.ffddp_solve_batch_dev.restype = C.c_int
+    lib.ffddp_calc_diff.argtypes = [C.c_void_p, C.c_int, dp, dp, dp, up, dp, dp] + [dp] * 10
+    lib.ffddp_calc_diff.restype = C.c_int
+    lib.ffddp_frame_placement.argtypes = [C.POINTER(Robot), dp, dp, dp]
+    lib.ffddp_frame_placement.restype = C.c_int
+    lib.ffddp_gravity_torque.argtypes = [C.POINTER(Robot), C.c_int, dp, dp]
+    lib.ffddp_gravity_torque.restype = C.c_int
+    lib.ffddp_gravity_torque_dev.argtypes = [C.c_void_p, C.c_int, vp, vp, vp]
+    lib.ffddp_gravity_torque_dev.restype = C.c_int
+    _lib = lib
+    return lib
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def iptr(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def uptr(a: np.ndarray):
+    assert a.dtype == np.uint8 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+_ROBOT = None
+
+
+def robot_struct() -> Robot:
+    global _ROBOT
+    if _ROBOT is None:
+        _ROBOT = make_robot()
+    return _ROBOT
+
+
+def frame_placement(q) -> tuple[np.ndarray, np.ndarray]:
+    """EE placement (R, p) on the host via the library's model code."""
+    lib = load()
+    q = np.ascontiguousarray(q, dtype=np.float64).reshape(7)
+    Rm = np.zeros(9)
+    p = np.zeros(3)
+    rc = lib.ffddp_frame_placement(C.byref(robot_struct()), dptr(q), dptr(Rm), dptr(p))
+    if rc:
+        raise RuntimeError(f"ffddp_frame_placement failed ({rc})")
+    return Rm.reshape(3, 3), p
+
+
+def gravity_torque(q) -> np.ndarray:
+    """rnea(q, 0, 0) for a batch (B,7) on the host via the library's model code."""
+    lib = load()
+    q = np.ascontiguousarray(np.atleast_2d(q), dtype=np.float64)
+    out = np.zeros_like(q)
+    rc = lib.ffddp_gravity_torque(C.byref(robot_struct()), q.shape[0], dptr(q), dptr(out))
+    if rc:
+        raise RuntimeError(f"ffddp_gravity_torque failed ({rc})")
+    return out

@@ -1,0 +1,126 @@
+"""Crocoddyl-like solver surface over the batched HIP (Box)FDDP.
+
+Mirrors what the reference uses of crocoddyl.SolverBoxFDDP
+(crocoddyl_classical.py:350-388, 442-445; crocoddyl_force_feedback.py:588-628):
+
+    solver = BatchedBoxFDDP(cfg, max_batch)            # SolverBoxFDDP(problem)
+    ok = solver.solve(batch, maxiter=10, is_feasible=False)   # solver.solve(...)
+    solver.xs, solver.us, solver.K, solver.cost, solver.iter  # read-backs
+
+with a leading batch axis.  Numerical failure never raises (ok[b] = False,
+like Crocoddyl); API / device errors raise RuntimeError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from .config import OcpConfig
+
+
+class FfddpError(RuntimeError):
+    pass
+
+
+class BatchedBoxFDDP:
+    def __init__(self, cfg: OcpConfig, max_batch: int, device: int = 0):
+        self.cfg = cfg
+        self.N = int(cfg.horizon)
+        self.nx = cfg.nx
+        self.nu = 7
+        self.max_batch = int(max_batch)
+        self._lib = _abi.load()
+        self._cfg_struct = cfg.to_struct()
+        h = C.c_void_p()
+        rc = self._lib.ffddp_create(
+            C.byref(_abi.robot_struct()), C.byref(self._cfg_struct), int(device), self.max_batch, C.byref(h)
+        )
+        if rc != 0:
+            raise FfddpError(f"ffddp_create failed with code {rc}")
+        self._h = h
+        self.xs = self.us = self.K = self.cost = self.iter = self.ok = self.fn_pred = self.stats = None
+
+    # -- lifecycle ------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.ffddp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self._lib.ffddp_last_error(self._h)
+            raise FfddpError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    # -- solve (host arrays) ----------------------------------------------------------
+    def solve(self, batch, maxiter: int = 10, is_feasible: bool = False, xs_init=None, us_init=None):
+        """batch: workload.Batch (or any object with x0, node_ref, inst_ref, surface,
+        xs_init, us_init).  Returns ok (B,) bool."""
+        B = int(batch.x0.shape[0])
+        N, nx = self.N, self.nx
+        f = lambda a, shape: np.ascontiguousarray(np.asarray(a, np.float64).reshape(shape))
+        x0 = f(batch.x0, (B, nx))
+        nref = f(batch.node_ref, (B, N + 1, 6))
+        iref = f(batch.inst_ref, (B, 21))
+        surf = np.ascontiguousarray(np.asarray(batch.surface, np.uint8).reshape(B))
+        xsi = f(batch.xs_init if xs_init is None else xs_init, (B, N + 1, nx))
+        usi = f(batch.us_init if us_init is None else us_init, (B, N, 7))
+        xs = np.zeros((B, N + 1, nx))
+        us = np.zeros((B, N, 7))
+        K = np.zeros((B, N, 7, nx))
+        cost = np.zeros(B)
+        iters = np.zeros(B, np.int32)
+        ok = np.zeros(B, np.uint8)
+        fn = np.zeros((B, 2))
+        stats = np.zeros((B, 4), np.int32)
+        d, i, u = _abi.dptr, _abi.iptr, _abi.uptr
+        rc = self._lib.ffddp_solve_batch(
+            self._h, B, d(x0), d(nref), d(iref), u(surf), d(xsi), d(usi), int(maxiter), int(bool(is_feasible)),
+            d(xs), d(us), d(K), d(cost), i(iters), u(ok), d(fn), i(stats),
+        )
+        self._check(rc, "ffddp_solve_batch")
+        self.xs, self.us, self.K, self.cost, self.iter = xs, us, K, cost, iters
+        self.ok, self.fn_pred, self.stats = ok.astype(bool), fn, stats
+        return self.ok
+
+    # -- solve (device-resident torch tensors; bench path) ---------------------------
+    def solve_dev(self, t, maxiter: int = 10, is_feasible: bool = False, stream=None):
+        """t: dict of contiguous torch.cuda tensors with keys x0, node_ref, inst_ref,
+        surface (uint8), xs_init, us_init and outputs xs, us, K, cost, iters (int32),
+        ok (uint8), fn_pred, stats (int32).  Asynchronous on `stream` (hipStream_t int)."""
+        B = int(t["x0"].shape[0])
+        p = lambda k: C.c_void_p(int(t[k].data_ptr()))
+        rc = self._lib.ffddp_solve_batch_dev(
+            self._h, B, p("x0"), p("node_ref"), p("inst_ref"), p("surface"), p("xs_init"), p("us_init"),
+            int(maxiter), int(bool(is_feasible)), p("xs"), p("us"), p("K"), p("cost"), p("iters"), p("ok"),
+            p("fn_pred"), p("stats"), C.c_void_p(stream if stream else 0),
+        )
+        self._check(rc, "ffddp_solve_batch_dev")
+
+    # -- problem.calcDiff(xs, us) -------------------------------------------------------
+    def calc_diff(self, batch, xs, us):
+        B = int(batch.x0.shape[0])
+        N, nx = self.N, self.nx
+        f = lambda a, shape: np.ascontiguousarray(np.asarray(a, np.float64).reshape(shape))
+        out = dict(
+            Fx=np.zeros((B, N, nx, nx)), Fu=np.zeros((B, N, nx, 7)), Lx=np.zeros((B, N + 1, nx)),
+            Lu=np.zeros((B, N, 7)), Lxx=np.zeros((B, N + 1, nx, nx)), Lxu=np.zeros((B, N, nx, 7)),
+            Luu=np.zeros((B, N, 7, 7)), cost=np.zeros((B, N + 1)), xnext=np.zeros((B, N, nx)),
+            lam=np.zeros((B, N + 1, 3)),
+        )
+        d = _abi.dptr
+        rc = self._lib.ffddp_calc_diff(
+            self._h, B, d(f(batch.x0, (B, nx))), d(f(batch.node_ref, (B, N + 1, 6))), d(f(batch.inst_ref, (B, 21))),
+            _abi.uptr(np.ascontiguousarray(np.asarray(batch.surface, np.uint8))), d(f(xs, (B, N + 1, nx))),
+            d(f(us, (B, N, 7))), d(out["Fx"]), d(out["Fu"]), d(out["Lx"]), d(out["Lu"]), d(out["Lxx"]),
+            d(out["Lxu"]), d(out["Luu"]), d(out["cost"]), d(out["xnext"]), d(out["lam"]),
+        )
+        self._check(rc, "ffddp_calc_diff")
+        return out

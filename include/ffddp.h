@@ -1,0 +1,154 @@
+/*
+ * ffddp.h — C-ABI of the MI355X-native batched (Box)FDDP solver.
+ *
+ * Drop-in boundary for the reference's hot path
+ *     ok = solver.solve(xs_init, us_init, max_iters, False)
+ * at src/mpc/crocoddyl_classical.py:367 (ClassicalCrocoddylMPC) and
+ * src/mpc/crocoddyl_force_feedback.py:605 (ForceFeedbackCrocoddylMPC), where
+ * `solver` is crocoddyl.SolverBoxFDDP(problem) (crocoddyl_classical.py:442-445)
+ * over the ShootingProblem built by _build_problem (:521-556 / FF :776-836).
+ * The reference binds Crocoddyl through boost-python; this library is bound
+ * through ctypes.  Plain pointers and sizes only.
+ *
+ * Conventions
+ *   - fp64 everywhere; all matrices row-major.
+ *   - One handle = one OCP definition (robot + weights + horizon + variant),
+ *     bound to one HIP device.  A handle is not thread-safe.
+ *   - Return 0 on success or a negative FFDDP_E* code for API / launch / OOM
+ *     errors.  Per-instance numerical failure is reported in ok[b] = 0 (the
+ *     cost may be NaN), exactly like Crocoddyl's solve() returning False.
+ *   - No C++ exception crosses this boundary.
+ */
+#ifndef FFDDP_H_
+#define FFDDP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FFDDP_NQ 7      /* Panda arm joints (fingers locked, crocoddyl_classical.py:189-197) */
+#define FFDDP_NU 7      /* ActuationModelFull: nu = nv (:147) */
+#define FFDDP_MAX_NC 3  /* ContactModel1D (nc=1) or ContactModel3D (nc=3) */
+
+enum {
+  FFDDP_OK = 0,
+  FFDDP_E_INVALID = -1,  /* bad argument (sizes, null pointers, config) */
+  FFDDP_E_DEVICE = -2,   /* HIP runtime / launch error */
+  FFDDP_E_OOM = -3,      /* device allocation failed */
+  FFDDP_E_CAPACITY = -4  /* B larger than the handle's max_batch */
+};
+
+enum { FFDDP_CLASSICAL = 0, FFDDP_FORCE_FEEDBACK = 1 };
+
+/* Rigid-body model of the 7-DoF arm: revolute-z joints in a serial chain.
+ * Replaces example_robot_data.load("panda") + pin.buildReducedModel
+ * (crocoddyl_classical.py:137-145, 189-197). */
+typedef struct ffddp_robot {
+  double joint_R[FFDDP_NQ][9]; /* placement of joint i in its parent (rotation) */
+  double joint_p[FFDDP_NQ][3]; /* placement of joint i in its parent (translation) */
+  double mass[FFDDP_NQ];
+  double com[FFDDP_NQ][3];     /* COM in the link frame */
+  double inertia[FFDDP_NQ][9]; /* rotational inertia about the COM, link frame */
+  double ee_R[9];              /* EE frame ("panda_link8") in link 7 */
+  double ee_p[3];
+  double gravity[3];           /* world gravity, (0,0,-9.81) */
+} ffddp_robot;
+
+/* OCP definition: every field the reference's _build_problem/_make_dam reads
+ * from ClassicalMPCConfig / ForceFeedbackMPCConfig
+ * (crocoddyl_classical.py:12-110, 521-728; crocoddyl_force_feedback.py:12-146,
+ * 149-290, 776-1009).  Costs with weight 0 are not added (as in the reference). */
+typedef struct ffddp_ocp_config {
+  int32_t variant;      /* FFDDP_CLASSICAL (nx=14) or FFDDP_FORCE_FEEDBACK (nx=21) */
+  int32_t horizon;      /* N running nodes + 1 terminal node */
+  int32_t nc;           /* 1 = ContactModel1D normal_1d, 3 = ContactModel3D point3d */
+  int32_t use_box;      /* 1 = SolverBoxFDDP (default), 0 = SolverFDDP */
+  double dt;            /* dt_ocp */
+  double z_press;
+  double w_ee_pos, w_ee_ori;
+  double ori_weights[3];
+  double w_posture, w_v;
+  double v_damp_weights[7];
+  double w_tau, w_tau_soft_limits, tau_soft_limit_margin;
+  double w_q_soft_limits, q_soft_limit_margin;
+  double q_lower[7], q_upper[7];
+  double w_tangent_pos, w_tangent_vel, w_plane_z, w_vz;
+  double w_unilateral, friction_margin, w_fn, fn_des;
+  double w_wdamp;
+  double w_wdamp_weights[3];
+  double contact_gains[2];   /* Baumgarte [Kp, Kd] */
+  double contact_inv_damping;/* JMinvJt_damping */
+  double tau_limits[7];      /* u_lb = -tau_limits, u_ub = +tau_limits */
+  double R_des[9];           /* FrameRotation reference, Pinocchio world */
+  /* force-feedback augmentation (_AugmentedLPFActionModel) */
+  double ff_alpha;           /* tau_{k+1} = alpha tau_k + (1-alpha) w_k */
+  double w_w, w_w_soft_limits, w_y;
+  double y_weights[21];
+  int32_t use_inner_state_reg, use_inner_tau_reg;
+} ffddp_ocp_config;
+
+typedef struct ffddp_handle ffddp_handle;
+
+/* crocoddyl.SolverBoxFDDP(problem) / setProblem (crocoddyl_classical.py:350-361):
+ * allocates device workspace for up to max_batch instances. */
+int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int device,
+                 int max_batch, ffddp_handle** out);
+void ffddp_destroy(ffddp_handle* h);
+const char* ffddp_last_error(const ffddp_handle* h);
+
+/* Batched solver.solve(xs_init, us_init, maxiter, is_feasible)
+ * (crocoddyl_classical.py:365-388, crocoddyl_force_feedback.py:603-628).
+ * Host pointers, row-major:
+ *   x0       [B][nx]           problem.x0 (FF: y0 = [q, v, tau_hat])
+ *   node_ref [B][N+1][6]       p_ref, v_ref per node, Pinocchio world (:526-546)
+ *   inst_ref [B][21]           x_reg_ref (14), tau_ref (7)           (:523-524)
+ *   surface  [B]               0 free-space DAM, 1 contact DAM       (:533, 614)
+ *   xs_init  [B][N+1][nx], us_init [B][N][7]                         (:365)
+ * Outputs (solver.xs, solver.us, solver.K, solver.cost, solver.iter, ok):
+ *   xs [B][N+1][nx], us [B][N][7], K [B][N][7][nx], cost [B], iters [B], ok [B]
+ *   fn_pred [B][2]   contact lambda_normal at knots 0 and 1 of the solution
+ *                    (crocoddyl_classical.py:905-942, FF :1219-1299; NaN if free)
+ *   stats  [B][4]    (optional, may be NULL) per instance: iterations run,
+ *                    sequential-equivalent line-search trials, regularisation
+ *                    retries, backward passes — for the roofline byte count. */
+int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* node_ref,
+                      const double* inst_ref, const uint8_t* surface, const double* xs_init,
+                      const double* us_init, int maxiter, int is_feasible, double* xs, double* us,
+                      double* K, double* cost, int32_t* iters, uint8_t* ok, double* fn_pred,
+                      int32_t* stats);
+
+/* Same with DEVICE pointers (inputs resident in HBM) on `stream` (hipStream_t,
+ * NULL = default stream).  Asynchronous: the caller synchronises the stream. */
+int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double* node_ref,
+                          const double* inst_ref, const uint8_t* surface, const double* xs_init,
+                          const double* us_init, int maxiter, int is_feasible, double* xs,
+                          double* us, double* K, double* cost, int32_t* iters, uint8_t* ok,
+                          double* fn_pred, int32_t* stats, void* stream);
+
+/* problem.calcDiff(xs, us) on the device (ShootingProblem::calcDiff; used by
+ * parity tests of the per-node models).  Host pointers.  Outputs per node in
+ * Crocoddyl layout (running nodes t < N, terminal node t = N):
+ *   Fx [B][N][nx][nx], Fu [B][N][nx][7], Lx [B][N+1][nx], Lu [B][N][7],
+ *   Lxx [B][N+1][nx][nx], Lxu [B][N][nx][7], Luu [B][N][7][7],
+ *   cost [B][N+1], xnext [B][N][nx], lam [B][N+1][3] (contact force, 0 if free). */
+int ffddp_calc_diff(ffddp_handle* h, int B, const double* x0, const double* node_ref,
+                    const double* inst_ref, const uint8_t* surface, const double* xs,
+                    const double* us, double* Fx, double* Fu, double* Lx, double* Lu, double* Lxx,
+                    double* Lxu, double* Luu, double* cost, double* xnext, double* lam);
+
+/* Host-side setup helpers (CPU, same model code): frame placement of the EE
+ * (pin.forwardKinematics + updateFramePlacements, crocoddyl_classical.py:199-225)
+ * and gravity torque rnea(q, 0, 0) (_gravity_torque, :447-451) for B configurations. */
+int ffddp_frame_placement(const ffddp_robot* robot, const double* q, double* R, double* p);
+int ffddp_gravity_torque(const ffddp_robot* robot, int B, const double* q, double* tau);
+
+/* Batched gravity torque on the device (tau_ref for B instances), device pointers. */
+int ffddp_gravity_torque_dev(ffddp_handle* h, int B, const double* q, double* tau, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FFDDP_H_ */
