@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""Benchmark: batched Franka 7-DoF horizon-30 (Box)FDDP solves/s on MI355X.
+
+BASELINE.json metric: "FDDP solves/sec, Franka 7-DoF horizon-30 batch=4096,
+at 1/2/4/8 MI355X".  One step = one solver.solve(xs_init, us_init, 10, False)
+(crocoddyl_classical.py:367) for a batch of B synthetic OCP instances per GPU
+(classical nx=14 nu=7, contact model normal_1d, cold warm start), inputs
+already resident in HBM.  N GPUs = N independent shards (one process per GPU,
+weak scaling); the only collective is the final all-gather of per-instance
+costs and first controls (RCCL, the exchange the north star names).
+
+Prints ONE JSON line (rank 0).  Extra objects:
+  roofline      dominant kernel's algorithmic bytes per launch / its average
+                HIP-event-timed launch duration, vs 8 TB/s.
+  cpu_baseline  the numpy oracle (oracle/, the CPU restatement) timed on a
+                bounded sample of the same workload on one host core.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+import ffddp_path  # noqa: E402,F401
+
+import numpy as np  # noqa: E402
+
+METRIC = "FDDP solves/sec, Franka 7-DoF horizon-30 batch=4096, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_MEASURED_GBS = 6290.0  # float4 copy, same table
+FP64_VALU_PEAK_TFLOPS = 78.6  # AMD public MI355X vector fp64 spec
+
+
+def algorithmic_words(nx: int, nu: int, N: int):
+    """Per-node fp64 words of the staged calcDiff -> backward -> forward design
+    (SURVEY.md §8(d)): A = calcDiff (running node), B = backward, C = one
+    forward trial; *_T the terminal node; IO per solve."""
+    a_r = 2 * nx + nu + 6
+    a_w = 2 * nx * nx + 2 * nx * nu + nu * nu + 2 * nx + nu + 1
+    A = a_r + a_w
+    Bw = (a_w - 1) + nu * nx + nu + nx
+    Cf = 3 * nx + 2 * nu + nu * nx + 6 + nx + nu
+    A_T = (nx + 6) + (nx * nx + nx + 1)
+    B_T = nx * nx + 2 * nx
+    C_T = 4 * nx + 6
+    io = nx + (N + 1) * nx + N * nu + (N + 1) * 6 + 21 + (N + 1) * nx + N * nu + N * nu * nx + 1
+    return dict(A=A, B=Bw, C=Cf, A_T=A_T, B_T=B_T, C_T=C_T, IO=io)
+
+
+def kernel_bytes(stats: np.ndarray, nx: int, nu: int, N: int) -> dict:
+    """Algorithmic bytes of one solve of the whole batch, per kernel class."""
+    w = algorithmic_words(nx, nu, N)
+    n_calc = stats[:, 4].astype(np.float64)
+    n_bw = stats[:, 0].astype(np.float64)
+    n_trials = stats[:, 1].astype(np.float64)
+    return {
+        "node": 8.0 * float(np.sum(n_calc)) * (N * w["A"] + w["A_T"]),
+        "backward": 8.0 * float(np.sum(n_bw)) * (N * w["B"] + w["B_T"]),
+        "forward": 8.0 * float(np.sum(n_trials)) * (N * w["C"] + w["C_T"]),
+        "io": 8.0 * stats.shape[0] * w["IO"],
+    }
+
+
+def cpu_baseline(cfg, batch, budget_s: float = 12.0, max_inst: int = 64) -> dict:
+    """Oracle (numpy fp64 restatement) on one core over a bounded sample of
+    the same instances.  Test infrastructure used only as the baseline leg."""
+    from oracle import fddp, ocp  # noqa: WPS433 (checker import, baseline leg only)
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    from helpers import oracle_cfg  # noqa: E402
+
+    ocfg = oracle_cfg(cfg)
+    t0 = time.perf_counter()
+    n = 0
+    for i in range(min(max_inst, batch.B)):
+        prob = ocp.Problem(
+            batch.x0[i], batch.node_ref[i, :, :3], batch.node_ref[i, :, 3:], batch.inst_ref[i, :14],
+            batch.inst_ref[i, 14:], bool(batch.surface[i]),
+        )
+        s = fddp.SolverBoxFDDP(ocfg, prob)
+        s.solve(batch.xs_init[i], batch.us_init[i], 10, False)
+        n += 1
+        if time.perf_counter() - t0 > budget_s and n >= 4:
+            break
+    dt = time.perf_counter() - t0
+    return {
+        "value": n / dt,
+        "unit": "solves/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {n} instances of the rank-0 batch (same seed/workload), numpy oracle, maxiter=10, "
+        f"{dt:.1f} s on 1 host thread",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--horizon", type=int, default=30)
+    ap.add_argument("--variant", choices=("classical", "ff"), default="classical")
+    ap.add_argument("--contact", choices=("normal_1d", "point3d"), default="normal_1d")
+    ap.add_argument("--maxiter", type=int, default=10)
+    ap.add_argument("--regime", choices=("tracking", "random"), default="tracking")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP-event timing")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from ffddp import BatchedBoxFDDP, _abi, robot as R, workload
+    from ffddp.config import classical_preset, ff_preset
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    B, N = args.batch, args.horizon
+    cfg = ff_preset(N, args.contact) if args.variant == "ff" else classical_preset(N, args.contact)
+    nx, nu = cfg.nx, 7
+    ee = R.R_MJ_FROM_PIN @ _abi.frame_placement(R.Q_NEUTRAL)[1]
+    batch = workload.make_batch(
+        B, N, args.variant, _abi.gravity_torque, ee, seed=1234 + rank, regime=args.regime, fk=_abi.frame_placement
+    )
+    f64 = dict(dtype=torch.float64, device=dev)
+    T = dict(
+        x0=torch.tensor(batch.x0, **f64),
+        node_ref=torch.tensor(batch.node_ref, **f64),
+        inst_ref=torch.tensor(batch.inst_ref, **f64),
+        surface=torch.tensor(batch.surface, dtype=torch.uint8, device=dev),
+        xs_init=torch.tensor(batch.xs_init, **f64),
+        us_init=torch.tensor(batch.us_init, **f64),
+        xs=torch.zeros((B, N + 1, nx), **f64),
+        us=torch.zeros((B, N, nu), **f64),
+        K=torch.zeros((B, N, nu, nx), **f64),
+        cost=torch.zeros(B, **f64),
+        iters=torch.zeros(B, dtype=torch.int32, device=dev),
+        ok=torch.zeros(B, dtype=torch.uint8, device=dev),
+        fn_pred=torch.zeros((B, 2), **f64),
+        stats=torch.zeros((B, _abi.NSTATS), dtype=torch.int32, device=dev),
+    )
+    solver = BatchedBoxFDDP(cfg, max_batch=B, device=local_rank)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    gathered = torch.zeros((world, B, 1 + nu), **f64) if world > 1 else None
+
+    def step():
+        solver.solve_dev(T, maxiter=args.maxiter, is_feasible=False, stream=stream)
+        if world > 1:  # final exchange: per-instance cost + first control to every rank
+            local = torch.cat([T["cost"][:, None], T["us"][:, 0, :]], 1)
+            dist.all_gather_into_tensor(gathered, local)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if not args.no_profile:
+        solver.profile(True)
+        solver.profile_read(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = solver.profile_read(reset=True) if not args.no_profile else None
+
+    stats = T["stats"].cpu().numpy()
+    ok = T["ok"].cpu().numpy()
+    iters = T["iters"].cpu().numpy()
+    cost = T["cost"].cpu().numpy()
+    total = B * world * args.steps
+    value = total / elapsed
+
+    roofline = None
+    kernels = None
+    if prof is not None:
+        kb = kernel_bytes(stats, nx, nu, N)
+        kernels = {k: {"ms_per_step": v[0] / args.steps, "launches_per_step": v[1] / args.steps} for k, v in prof.items()}
+        dom = max(("node", "backward", "forward"), key=lambda k: prof[k][0])
+        ms, launches = prof[dom]
+        avg_launch_s = ms / 1e3 / max(1, launches)
+        bytes_per_launch = kb[dom] * args.steps / max(1, launches)
+        achieved = bytes_per_launch / avg_launch_s / 1e9
+        traffic = None
+        tf = ROOT / "profiles" / "traffic_latest.json"
+        if tf.exists():
+            try:
+                tj = json.loads(tf.read_text())
+                if tj.get("kernel") == dom and tj.get("config") == f"{args.variant}/{args.contact}/B{B}/N{N}":
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "bytes_per_launch": bytes_per_launch,
+            "avg_launch_ms": avg_launch_s * 1e3,
+            "frac_of_measured_copy": achieved / HBM_MEASURED_GBS,
+        }
+
+    if rank == 0:
+        base = None
+        if not args.no_cpu_baseline and world == 1:
+            base = cpu_baseline(cfg, batch, budget_s=args.cpu_budget)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded workload.make_batch, tracking regime: x0 near IK of the benchmark "
+            "trajectory at t0~U(0,20)s; cold warm start)",
+            "config": {
+                "workload": f"{args.variant} BoxFDDP solve, nx={nx} nu={nu}, horizon={N}, batch={B}/GPU, "
+                f"maxiter={args.maxiter}, contact={args.contact}",
+                "variant": args.variant,
+                "horizon": N,
+                "batch_per_gpu": B,
+                "global_batch": B * world,
+                "maxiter": args.maxiter,
+                "contact_model": args.contact,
+                "parallelism": f"shard{world}",
+            },
+            "roofline": roofline,
+            "cpu_baseline": base,
+            "solver": {
+                "ok_frac": float(np.mean(ok)),
+                "mean_iter": float(np.mean(iters)),
+                "mean_iters_run": float(np.mean(stats[:, 0])),
+                "mean_trials": float(np.mean(stats[:, 1])),
+                "cost_finite_frac": float(np.mean(np.isfinite(cost))),
+            },
+            "kernels": kernels,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -40,7 +40,7 @@ constexpr int FW_BLOCK = 64;
 struct InstState {
   double preg, cost, dg, dq, stop;
   int is_feasible, was_feasible, done, ok, iter, recalc, accepted, bw_ok;
-  int n_iters, n_trials, n_retries, n_backward;
+  int n_iters, n_trials, n_retries, n_backward, n_calc, n_forward;
 };
 
 struct Dev {
@@ -90,7 +90,7 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
       s.recalc = 1;
       s.accepted = -1;
       s.bw_ok = 0;
-      s.n_iters = s.n_trials = s.n_retries = s.n_backward = 0;
+      s.n_iters = s.n_trials = s.n_retries = s.n_backward = s.n_calc = s.n_forward = 0;
       d.st[i] = s;
     }
   }
@@ -452,6 +452,7 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
   const double* recb = d.rec_buf + (long)b * (N + 1) * d.rec;
   // total cost from the fresh calc (ShootingProblem::calcDiff sum, t = 0..N)
   if (st->recalc && tid == 0) {
+    st->n_calc += 1;
     double c = 0.0;
     for (int t = 0; t <= N; ++t) c += recb[(long)t * d.rec + rec_off_cost(nx)];
     st->cost = c;
@@ -840,6 +841,7 @@ __global__ void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter) {
   }
   if (acc < 0) s.recalc = 0;  // (xs, us) unchanged: node data stays valid
   s.n_trials += tried;
+  s.n_forward += 1;
   s.accepted = acc;
   if (steplength > C.th_stepdec) s.preg = fmax(s.preg / C.reg_dec, C.reg_min);
   if (steplength <= C.th_stepinc) {
@@ -891,10 +893,12 @@ __global__ __launch_bounds__(64) void k_finalize(const DevConsts* __restrict__ C
     iters[b] = s.done ? s.iter : maxiter;
     ok[b] = (s.done && s.ok) ? 1 : 0;
     if (stats) {
-      stats[(long)b * 4 + 0] = s.n_iters;
-      stats[(long)b * 4 + 1] = s.n_trials;
-      stats[(long)b * 4 + 2] = s.n_retries;
-      stats[(long)b * 4 + 3] = s.n_backward;
+      stats[(long)b * FFDDP_NSTATS + 0] = s.n_iters;
+      stats[(long)b * FFDDP_NSTATS + 1] = s.n_trials;
+      stats[(long)b * FFDDP_NSTATS + 2] = s.n_retries;
+      stats[(long)b * FFDDP_NSTATS + 3] = s.n_backward;
+      stats[(long)b * FFDDP_NSTATS + 4] = s.n_calc;
+      stats[(long)b * FFDDP_NSTATS + 5] = s.n_forward;
     }
   }
   if (fn_pred == nullptr) return;
@@ -939,6 +943,13 @@ struct ffddp_handle {
   int32_t *out_iters = nullptr, *out_stats = nullptr;
   uint8_t* out_ok = nullptr;
   std::string err;
+  // optional per-kernel timing
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<int> ev_class;  // class per event pair
+  double prof_ms[FFDDP_NKERNELS] = {0};
+  int64_t prof_n[FFDDP_NKERNELS] = {0};
 };
 
 namespace {
@@ -1092,6 +1103,31 @@ void free_all(ffddp_handle* h) {
     if (p) (void)hipFree(p);
 }
 
+// event pair around a launch (only when profiling is enabled)
+struct ProfScope {
+  ffddp_handle* h;
+  hipStream_t s;
+  ProfScope(ffddp_handle* h_, hipStream_t s_, int cls) : h(h_), s(s_) {
+    if (!h->prof) return;
+    if (h->ev_used + 2 > h->ev_pool.size()) {
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        h->ev_pool.push_back(e);
+      }
+    }
+    h->ev_class.push_back(cls);
+    (void)hipEventRecord(h->ev_pool[h->ev_used], s);
+  }
+  ~ProfScope() {
+    if (!h->prof) return;
+    (void)hipEventRecord(h->ev_pool[h->ev_used + 1], s);
+    h->ev_used += 2;
+  }
+};
+
+enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE };
+
 template <int NC, bool FF>
 int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref, const double* iref,
                  const uint8_t* surf, const double* xs_init, const double* us_init, int maxiter, int is_feasible,
@@ -1100,19 +1136,40 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
   Dev d = h->d;
   d.B = B;
   const int N = h->hc.N, nx = h->hc.nx;
-  hipLaunchKernelGGL(k_init, dim3(1024), dim3(256), 0, s, h->dc, d, xs_init, us_init, is_feasible);
+  {
+    ProfScope p(h, s, KC_INIT);
+    hipLaunchKernelGGL(k_init, dim3(1024), dim3(256), 0, s, h->dc, d, xs_init, us_init, is_feasible);
+  }
   const long nodes = (long)B * (N + 1);
   const int node_blocks = (int)((nodes + NODE_GPB - 1) / NODE_GPB);
   const int fw_blocks = (int)(((long)B * NTRIALS + FW_BLOCK - 1) / FW_BLOCK);
   for (int it = 0; it < maxiter; ++it) {
-    hipLaunchKernelGGL((k_node<NC, FF>), dim3(node_blocks), dim3(NODE_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf, 0);
-    hipLaunchKernelGGL((k_backward<FF>), dim3(B), dim3(BW_BLOCK), 0, s, h->dc, d, it);
-    hipLaunchKernelGGL((k_forward<NC, FF>), dim3(fw_blocks), dim3(FW_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf);
-    hipLaunchKernelGGL(k_accept, dim3((B + 255) / 256), dim3(256), 0, s, h->dc, d, it);
-    hipLaunchKernelGGL(k_commit, dim3(2048), dim3(256), 0, s, h->dc, d);
+    {
+      ProfScope p(h, s, KC_NODE);
+      hipLaunchKernelGGL((k_node<NC, FF>), dim3(node_blocks), dim3(NODE_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf, 0);
+    }
+    {
+      ProfScope p(h, s, KC_BACKWARD);
+      hipLaunchKernelGGL((k_backward<FF>), dim3(B), dim3(BW_BLOCK), 0, s, h->dc, d, it);
+    }
+    {
+      ProfScope p(h, s, KC_FORWARD);
+      hipLaunchKernelGGL((k_forward<NC, FF>), dim3(fw_blocks), dim3(FW_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf);
+    }
+    {
+      ProfScope p(h, s, KC_ACCEPT);
+      hipLaunchKernelGGL(k_accept, dim3((B + 255) / 256), dim3(256), 0, s, h->dc, d, it);
+    }
+    {
+      ProfScope p(h, s, KC_COMMIT);
+      hipLaunchKernelGGL(k_commit, dim3(2048), dim3(256), 0, s, h->dc, d);
+    }
   }
-  hipLaunchKernelGGL((k_finalize<NC, FF>), dim3((2 * B + 63) / 64), dim3(64), 0, s, h->dc, d, maxiter, x0, nref, iref,
-                     surf, cost, iters, ok, fn_pred, stats);
+  {
+    ProfScope p(h, s, KC_FINALIZE);
+    hipLaunchKernelGGL((k_finalize<NC, FF>), dim3((2 * B + 63) / 64), dim3(64), 0, s, h->dc, d, maxiter, x0, nref,
+                       iref, surf, cost, iters, ok, fn_pred, stats);
+  }
   if (hipGetLastError() != hipSuccess) return fail(h, FFDDP_E_DEVICE, "kernel launch failed");
   const size_t bx = (size_t)B * (N + 1) * nx * sizeof(double);
   const size_t bu = (size_t)B * N * NU * sizeof(double);
@@ -1198,7 +1255,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   rc |= dalloc(h, &h->out_cost, (size_t)B);
   rc |= dalloc(h, &h->out_fn, (size_t)B * 2);
   rc |= dalloc(h, &h->out_iters, (size_t)B);
-  rc |= dalloc(h, &h->out_stats, (size_t)B * 4);
+  rc |= dalloc(h, &h->out_stats, (size_t)B * FFDDP_NSTATS);
   rc |= dalloc(h, &h->out_ok, (size_t)B);
   if (rc) {
     free_all(h);
@@ -1215,9 +1272,40 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   return 0;
 }
 
+int ffddp_profile_enable(ffddp_handle* h, int on) {
+  if (!h) return FFDDP_E_INVALID;
+  h->prof = on != 0;
+  return 0;
+}
+
+int ffddp_profile_read(ffddp_handle* h, double* ms, int64_t* launches, int reset) {
+  if (!h) return FFDDP_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  for (size_t i = 0; i < h->ev_class.size(); ++i) {
+    hipEvent_t a = h->ev_pool[2 * i], b = h->ev_pool[2 * i + 1];
+    HIPCHK(h, hipEventSynchronize(b));
+    float t = 0.f;
+    HIPCHK(h, hipEventElapsedTime(&t, a, b));
+    h->prof_ms[h->ev_class[i]] += t;
+    h->prof_n[h->ev_class[i]] += 1;
+  }
+  h->ev_class.clear();
+  h->ev_used = 0;
+  for (int k = 0; k < FFDDP_NKERNELS; ++k) {
+    if (ms) ms[k] = h->prof_ms[k];
+    if (launches) launches[k] = h->prof_n[k];
+    if (reset) {
+      h->prof_ms[k] = 0.0;
+      h->prof_n[k] = 0;
+    }
+  }
+  return 0;
+}
+
 void ffddp_destroy(ffddp_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
+  for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   free_all(h);
   delete h;
 }
@@ -1270,7 +1358,7 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
   HIPCHK(h, hipMemcpy(iters, h->out_iters, (size_t)B * 4, hipMemcpyDeviceToHost));
   HIPCHK(h, hipMemcpy(ok, h->out_ok, (size_t)B, hipMemcpyDeviceToHost));
   if (fn_pred) HIPCHK(h, hipMemcpy(fn_pred, h->out_fn, (size_t)B * 2 * 8, hipMemcpyDeviceToHost));
-  if (stats) HIPCHK(h, hipMemcpy(stats, h->out_stats, (size_t)B * 4 * 4, hipMemcpyDeviceToHost));
+  if (stats) HIPCHK(h, hipMemcpy(stats, h->out_stats, (size_t)B * FFDDP_NSTATS * 4, hipMemcpyDeviceToHost));
   return 0;
 }
 

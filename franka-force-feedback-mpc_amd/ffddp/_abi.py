@@ -29,7 +29,11 @@ SYMBOLS = (
     "ffddp_frame_placement",
     "ffddp_gravity_torque",
     "ffddp_gravity_torque_dev",
+    "ffddp_profile_enable",
+    "ffddp_profile_read",
 )
+NSTATS = 6
+KERNEL_CLASSES = ("init", "node", "backward", "forward", "accept", "commit", "finalize")
 
 
 class Robot(C.Structure):
@@ -154,6 +158,10 @@ def load() -> C.CDLL:
     lib.ffddp_gravity_torque.restype = C.c_int
     lib.ffddp_gravity_torque_dev.argtypes = [C.c_void_p, C.c_int, vp, vp, vp]
     lib.ffddp_gravity_torque_dev.restype = C.c_int
+    lib.ffddp_profile_enable.argtypes = [C.c_void_p, C.c_int]
+    lib.ffddp_profile_enable.restype = C.c_int
+    lib.ffddp_profile_read.argtypes = [C.c_void_p, dp, C.POINTER(C.c_int64), C.c_int]
+    lib.ffddp_profile_read.restype = C.c_int
     _lib = lib
     return lib
 

@@ -79,7 +79,7 @@ class BatchedBoxFDDP:
         iters = np.zeros(B, np.int32)
         ok = np.zeros(B, np.uint8)
         fn = np.zeros((B, 2))
-        stats = np.zeros((B, 4), np.int32)
+        stats = np.zeros((B, _abi.NSTATS), np.int32)
         d, i, u = _abi.dptr, _abi.iptr, _abi.uptr
         rc = self._lib.ffddp_solve_batch(
             self._h, B, d(x0), d(nref), d(iref), u(surf), d(xsi), d(usi), int(maxiter), int(bool(is_feasible)),
@@ -103,6 +103,19 @@ class BatchedBoxFDDP:
             p("fn_pred"), p("stats"), C.c_void_p(stream if stream else 0),
         )
         self._check(rc, "ffddp_solve_batch_dev")
+
+    # -- per-kernel device timing ----------------------------------------------------
+    def profile(self, on: bool = True):
+        self._check(self._lib.ffddp_profile_enable(self._h, int(on)), "ffddp_profile_enable")
+
+    def profile_read(self, reset: bool = True) -> dict:
+        ms = np.zeros(len(_abi.KERNEL_CLASSES))
+        n = np.zeros(len(_abi.KERNEL_CLASSES), np.int64)
+        self._check(
+            self._lib.ffddp_profile_read(self._h, _abi.dptr(ms), n.ctypes.data_as(C.POINTER(C.c_int64)), int(reset)),
+            "ffddp_profile_read",
+        )
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(_abi.KERNEL_CLASSES)}
 
     # -- problem.calcDiff(xs, us) -------------------------------------------------------
     def calc_diff(self, batch, xs, us):

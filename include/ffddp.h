@@ -31,6 +31,8 @@ extern "C" {
 #define FFDDP_NQ 7      /* Panda arm joints (fingers locked, crocoddyl_classical.py:189-197) */
 #define FFDDP_NU 7      /* ActuationModelFull: nu = nv (:147) */
 #define FFDDP_MAX_NC 3  /* ContactModel1D (nc=1) or ContactModel3D (nc=3) */
+#define FFDDP_NSTATS 6  /* per-instance counters returned by the solve */
+#define FFDDP_NKERNELS 7 /* kernel classes reported by ffddp_profile_read */
 
 enum {
   FFDDP_OK = 0,
@@ -110,9 +112,13 @@ const char* ffddp_last_error(const ffddp_handle* h);
  *   xs [B][N+1][nx], us [B][N][7], K [B][N][7][nx], cost [B], iters [B], ok [B]
  *   fn_pred [B][2]   contact lambda_normal at knots 0 and 1 of the solution
  *                    (crocoddyl_classical.py:905-942, FF :1219-1299; NaN if free)
- *   stats  [B][4]    (optional, may be NULL) per instance: iterations run,
- *                    sequential-equivalent line-search trials, regularisation
- *                    retries, backward passes — for the roofline byte count. */
+ *   stats  [B][FFDDP_NSTATS]  (optional, may be NULL) per instance:
+ *                    [0] FDDP iterations with a successful backward pass,
+ *                    [1] line-search trials a sequential solver executes,
+ *                    [2] regularisation retries of the backward pass,
+ *                    [3] backward passes run, [4] calcDiff evaluations,
+ *                    [5] forward (line-search) launches — for the roofline
+ *                    byte count. */
 int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* node_ref,
                       const double* inst_ref, const uint8_t* surface, const double* xs_init,
                       const double* us_init, int maxiter, int is_feasible, double* xs, double* us,
@@ -143,6 +149,14 @@ int ffddp_calc_diff(ffddp_handle* h, int B, const double* x0, const double* node
  * and gravity torque rnea(q, 0, 0) (_gravity_torque, :447-451) for B configurations. */
 int ffddp_frame_placement(const ffddp_robot* robot, const double* q, double* R, double* p);
 int ffddp_gravity_torque(const ffddp_robot* robot, int B, const double* q, double* tau);
+
+/* Optional per-kernel device timing (HIP events recorded around every launch
+ * on the launch stream).  Kernel classes, in order: init, node (calc+calcDiff),
+ * backward, forward (line search), accept, commit, finalize.
+ * ffddp_profile_read synchronises the recorded events and returns, per class,
+ * the summed milliseconds and launch counts since the last reset. */
+int ffddp_profile_enable(ffddp_handle* h, int on);
+int ffddp_profile_read(ffddp_handle* h, double* ms, int64_t* launches, int reset);
 
 /* Batched gravity torque on the device (tau_ref for B instances), device pointers. */
 int ffddp_gravity_torque_dev(ffddp_handle* h, int B, const double* q, double* tau, void* stream);
