@@ -318,96 +318,72 @@ struct BwShared {
 
 __device__ __forceinline__ bool bad(double v) { return isnan(v) || isinf(v) || v >= 1e30; }
 
-// BoxQP (crocoddyl::BoxQP::solve), single lane.  H 7x7 (row-major), q, lb, ub,
-// x (in: warm start, out: solution), Hinv (free-block inverse scattered into
-// 7x7, zeros elsewhere), clamped flags.  Returns false on LLT failure.
-__device__ bool boxqp(const DevConsts& C, const double* H, const double* q, const double* lb, const double* ub,
-                      double* x, double* Hinv, int* clamped) {
+// BoxQP (crocoddyl::BoxQP::solve), one lane, everything in registers.
+// The free-set sub-problem is solved on the full 7x7 matrix with clamped
+// rows/columns replaced by identity rows (the same Cholesky as on H_ff); the
+// factorisation is reused while the free set does not change.
+// H (row-major 7x7), q, lb, ub; x: in = warm start, out = solution.
+// L: masked factor of the final free set (so that K = Quu_ff^-1 Qxu_f^T is
+// a masked solve), clamped: final clamped flags.  Returns false on LLT
+// failure ("backward_error").
+__device__ __forceinline__ bool boxqp_reg(const DevConsts& C, const double (&H)[NU * NU], const double (&q)[NU],
+                                          const double (&lb)[NU], const double (&ub)[NU], double (&x)[NU],
+                                          double (&L)[28], bool (&clamped)[NU]) {
+#pragma unroll
   for (int i = 0; i < NU; ++i) x[i] = fmax(fmin(x[i], ub[i]), lb[i]);
-  int freeI[NU], nf = NU;
+  bool have = false;
   for (int it = 0; it < C.qp_maxiter; ++it) {
     double g[NU];
+#pragma unroll
     for (int i = 0; i < NU; ++i) {
       double acc = q[i];
+#pragma unroll
       for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * x[j];
       g[i] = acc;
     }
-    nf = 0;
+    bool changed = !have;
+#pragma unroll
     for (int j = 0; j < NU; ++j) {
       const bool c = (x[j] == lb[j] && g[j] > 0.0) || (x[j] == ub[j] && g[j] < 0.0);
-      clamped[j] = c ? 1 : 0;
-      if (!c) freeI[nf++] = j;
+      changed |= (c != clamped[j]);
+      clamped[j] = c;
     }
-    double Lf[28];
-    for (int i = 0; i < nf; ++i)
-      for (int j = 0; j <= i; ++j) Lf[tri(i, j)] = H[freeI[i] * NU + freeI[j]] + ((i == j) ? C.qp_reg : 0.0);
-    // LLT
-    for (int j = 0; j < nf; ++j) {
-      double dd = Lf[tri(j, j)];
-      for (int k = 0; k < j; ++k) dd -= Lf[tri(j, k)] * Lf[tri(j, k)];
-      if (!(dd > 0.0)) return false;
-      const double l = sqrt(dd);
-      Lf[tri(j, j)] = l;
-      for (int i = j + 1; i < nf; ++i) {
-        double s = Lf[tri(i, j)];
-        for (int k = 0; k < j; ++k) s -= Lf[tri(i, k)] * Lf[tri(j, k)];
-        Lf[tri(i, j)] = s / l;
-      }
-    }
-    // Hff^-1 (scattered)
-    for (int i = 0; i < NU * NU; ++i) Hinv[i] = 0.0;
-    for (int c = 0; c < nf; ++c) {
-      double e[NU];
-      for (int i = 0; i < nf; ++i) e[i] = (i == c) ? 1.0 : 0.0;
-      for (int i = 0; i < nf; ++i) {
-        double s = e[i];
-        for (int k = 0; k < i; ++k) s -= Lf[tri(i, k)] * e[k];
-        e[i] = s / Lf[tri(i, i)];
-      }
-      for (int i = nf - 1; i >= 0; --i) {
-        double s = e[i];
-        for (int k = i + 1; k < nf; ++k) s -= Lf[tri(k, i)] * e[k];
-        e[i] = s / Lf[tri(i, i)];
-      }
-      for (int i = 0; i < nf; ++i) Hinv[freeI[i] * NU + freeI[c]] = e[i];
-    }
-    // Newton step on the free set
-    double dxf[NU];
-    for (int i = 0; i < nf; ++i) {
-      double acc = -q[freeI[i]];
-      for (int j = 0; j < NU; ++j)
-        if (clamped[j]) acc -= H[freeI[i] * NU + j] * x[j];
-      dxf[i] = acc;
-    }
-    for (int i = 0; i < nf; ++i) {
-      double s = dxf[i];
-      for (int k = 0; k < i; ++k) s -= Lf[tri(i, k)] * dxf[k];
-      dxf[i] = s / Lf[tri(i, i)];
-    }
-    for (int i = nf - 1; i >= 0; --i) {
-      double s = dxf[i];
-      for (int k = i + 1; k < nf; ++k) s -= Lf[tri(k, i)] * dxf[k];
-      dxf[i] = s / Lf[tri(i, i)];
+    if (changed) {
+#pragma unroll
+      for (int i = 0; i < NU; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j)
+          L[tri(i, j)] = (!clamped[i] && !clamped[j]) ? H[i * NU + j] + (i == j ? C.qp_reg : 0.0)
+                                                      : (i == j ? 1.0 : 0.0);
+      if (!chol_packed<NU>(L)) return false;
+      have = true;
     }
     double dx[NU];
-    for (int i = 0; i < NU; ++i) dx[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      double acc = -q[i];
+#pragma unroll
+      for (int j = 0; j < NU; ++j)
+        if (clamped[j]) acc -= H[i * NU + j] * x[j];
+      dx[i] = clamped[i] ? 0.0 : acc;
+    }
+    chol_solve<NU>(L, dx);
     double dmax = 0.0;
-    for (int i = 0; i < nf; ++i) {
-      dx[freeI[i]] = dxf[i] - x[freeI[i]];
-      dmax = fmax(dmax, fabs(dx[freeI[i]]));
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      dx[i] = clamped[i] ? 0.0 : dx[i] - x[i];
+      dmax = fmax(dmax, fabs(dx[i]));
     }
     if (dmax < C.qp_th_grad) break;
-    double Hx[NU];
-    double fold = 0.0;
-    for (int i = 0; i < NU; ++i) {
-      double acc = 0.0;
-      for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * x[j];
-      Hx[i] = acc;
-    }
+    double fold;
     {
       double a1 = 0.0, a2 = 0.0;
+#pragma unroll
       for (int i = 0; i < NU; ++i) {
-        a1 += x[i] * Hx[i];
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * x[j];
+        a1 += x[i] * acc;
         a2 += q[i] * x[i];
       }
       fold = 0.5 * a1 + a2;
@@ -415,23 +391,32 @@ __device__ bool boxqp(const DevConsts& C, const double* H, const double* q, cons
     for (int ia = 0; ia < NTRIALS; ++ia) {
       const double al = C.alphas[ia];
       double xn[NU];
+#pragma unroll
       for (int i = 0; i < NU; ++i) xn[i] = fmax(fmin(x[i] + al * dx[i], ub[i]), lb[i]);
       double a1 = 0.0, a2 = 0.0, gd = 0.0;
+#pragma unroll
       for (int i = 0; i < NU; ++i) {
         double acc = 0.0;
+#pragma unroll
         for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * xn[j];
         a1 += xn[i] * acc;
         a2 += q[i] * xn[i];
         gd += g[i] * (x[i] - xn[i]);
       }
-      const double fnew = 0.5 * a1 + a2;
-      if (fold - fnew > C.qp_th_acceptstep * gd) {
+      if (fold - (0.5 * a1 + a2) > C.qp_th_acceptstep * gd) {
+#pragma unroll
         for (int i = 0; i < NU; ++i) x[i] = xn[i];
         break;
       }
     }
   }
   return true;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
 }
 
 template <bool FF>
@@ -487,17 +472,15 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
         for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
         wN[i] = acc;
       }
-      if (tid == 0) {
-        double a1 = 0.0, a2 = 0.0;
-        for (int i = 0; i < nx; ++i) {
-          double acc = 0.0;
-          for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
-          a1 += S.Vx[i] * S.fs[i];
-          a2 += S.fs[i] * acc;
-        }
-        dg -= a1;
-        dq += a2;
+      double c1 = 0.0, c2 = 0.0;
+      if (tid < nx) {
+        double acc = 0.0;
+        for (int j = 0; j < nx; ++j) acc += S.Vxx[tid * nx + j] * S.fs[j];
+        c1 = S.Vx[tid] * S.fs[tid];
+        c2 = S.fs[tid] * acc;
       }
+      dg -= wave_sum(c1);
+      dq += wave_sum(c2);
     }
     bool failed = false;
     for (int t = N - 1; t >= 0; --t) {
@@ -572,26 +555,43 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
         S.Quu[tid] = acc;
       }
       __syncthreads();
-      // gains
+      // gains (one lane, registers)
       if (tid == 0) {
+        double H[NU * NU];
+#pragma unroll
+        for (int e = 0; e < NU * NU; ++e) H[e] = S.Quu[e];
         bool ok = true;
         if (!use_qp) {
+          double L[28];
+#pragma unroll
           for (int i = 0; i < NU; ++i)
-            for (int j = 0; j <= i; ++j) S.L[tri(i, j)] = S.Quu[i * NU + j];
-          ok = chol_packed<NU>(S.L);
+#pragma unroll
+            for (int j = 0; j <= i; ++j) L[tri(i, j)] = H[i * NU + j];
+          ok = chol_packed<NU>(L);
+#pragma unroll
+          for (int e = 0; e < 28; ++e) S.L[e] = L[e];
+#pragma unroll
           for (int i = 0; i < NU; ++i) S.clamped[i] = 0;
         } else {
-          double* kprev = d.k + ((long)b * N + t) * NU;
+          const double* kprev = d.k + ((long)b * N + t) * NU;
           const double* ut = d.us + ((long)b * N + t) * NU;
-          double lb[NU], ub[NU], x[NU], q[NU];
+          double lb[NU], ub[NU], x[NU], q[NU], L[28];
+          bool cl[NU] = {false, false, false, false, false, false, false};
+#pragma unroll
           for (int i = 0; i < NU; ++i) {
             lb[i] = C.u_lb[i] - ut[i];
             ub[i] = C.u_ub[i] - ut[i];
             x[i] = kprev[i];
             q[i] = S.Qu[i];
           }
-          ok = boxqp(C, S.Quu, q, lb, ub, x, S.Qinv, S.clamped);
-          for (int i = 0; i < NU; ++i) S.kk[i] = -x[i];
+          ok = boxqp_reg(C, H, q, lb, ub, x, L, cl);
+#pragma unroll
+          for (int e = 0; e < 28; ++e) S.L[e] = L[e];
+#pragma unroll
+          for (int i = 0; i < NU; ++i) {
+            S.kk[i] = -x[i];
+            S.clamped[i] = cl[i] ? 1 : 0;
+          }
         }
         S.flag = ok ? 0 : 1;
       }
@@ -600,26 +600,24 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
         failed = true;
         break;
       }
-      if (!use_qp) {
-        // K = Quu^-1 Qxu^T (one rhs per lane), k = Quu^-1 Qu
-        if (tid <= nx) {
-          double rhs[NU];
-          if (tid < nx)
-            for (int i = 0; i < NU; ++i) rhs[i] = S.Qxu[tid * NU + i];
-          else
-            for (int i = 0; i < NU; ++i) rhs[i] = S.Qu[i];
-          chol_solve<NU>(S.L, rhs);
-          if (tid < nx)
-            for (int i = 0; i < NU; ++i) S.K[i * nx + tid] = rhs[i];
-          else
-            for (int i = 0; i < NU; ++i) S.kk[i] = rhs[i];
+      // K = Quu^-1 Qxu^T, one rhs per lane (BoxQP: masked solve on the free set,
+      // i.e. Quu_inv restricted to the free block); LLT path: k = Quu^-1 Qu
+      if (tid < nx || (!use_qp && tid == nx)) {
+        double rhs[NU];
+        if (tid < nx) {
+#pragma unroll
+          for (int i = 0; i < NU; ++i) rhs[i] = S.clamped[i] ? 0.0 : S.Qxu[tid * NU + i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < NU; ++i) rhs[i] = S.Qu[i];
         }
-      } else {
-        for (int e = tid; e < NU * nx; e += BW_BLOCK) {
-          const int i = e / nx, j = e % nx;
-          double acc = 0.0;
-          for (int m = 0; m < NU; ++m) acc += S.Qinv[i * NU + m] * S.Qxu[j * NU + m];
-          S.K[e] = acc;
+        chol_solve<NU>(S.L, rhs);
+        if (tid < nx) {
+#pragma unroll
+          for (int i = 0; i < NU; ++i) S.K[i * nx + tid] = rhs[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < NU; ++i) S.kk[i] = rhs[i];
         }
       }
       __syncthreads();
@@ -667,30 +665,27 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
         failed = true;
         break;
       }
-      if (tid == 0) {
-        // expected-improvement partials (SolverFDDP::updateExpectedImprovement)
-        double qk = 0.0, kqk = 0.0, qu2 = 0.0;
-        for (int i = 0; i < NU; ++i) {
+      {
+        // expected-improvement partials (SolverFDDP::updateExpectedImprovement), wave-reduced
+        double c_dg = 0.0, c_dq = 0.0, c_st = 0.0;
+        if (tid < NU) {
           double quk = 0.0;
-          for (int j = 0; j < NU; ++j) quk += S.Quu[i * NU + j] * S.kk[j];
-          qk += S.Qu[i] * S.kk[i];
-          kqk += S.kk[i] * quk;
-          qu2 += S.Qu[i] * S.Qu[i];
+#pragma unroll
+          for (int j = 0; j < NU; ++j) quk += S.Quu[tid * NU + j] * S.kk[j];
+          c_dg += S.Qu[tid] * S.kk[tid];
+          c_dq -= S.kk[tid] * quk;
+          c_st += S.Qu[tid] * S.Qu[tid];
         }
-        dg += qk;
-        dq -= kqk;
-        stop += qu2;
-        if (!feas) {
-          double a1 = 0.0, a2 = 0.0;
-          for (int i = 0; i < nx; ++i) {
-            double acc = 0.0;
-            for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
-            a1 += S.Vx[i] * S.fs[i];
-            a2 += S.fs[i] * acc;
-          }
-          dg -= a1;
-          dq += a2;
+        if (!feas && tid < nx) {
+          c_dg -= S.Vx[tid] * S.fs[tid];
+          c_dq += S.fs[tid] * wt;
         }
+        c_dg = wave_sum(c_dg);
+        c_dq = wave_sum(c_dq);
+        c_st = wave_sum(c_st);
+        dg += c_dg;
+        dq += c_dq;
+        stop += c_st;
       }
     }
     if (!failed) {
@@ -826,8 +821,8 @@ __global__ void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter) {
     bool ok;
     if (dVexp >= 0)
       ok = fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp;
-    else
-      ok = fabs(d0) < C.th_grad || dV < C.th_acceptnegstep * dVexp;
+    else  // gap-closing branch: cost may rise by up to th_acceptnegstep x the prediction
+      ok = fabs(d0) < C.th_grad || dV > C.th_acceptnegstep * dVexp;
     if (ok) {
       acc = tr;
       steplength = a;

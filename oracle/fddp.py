@@ -131,28 +131,33 @@ class Stats:
 class SolverBoxFDDP:
     """Per-instance solver on one ocp.Problem (setProblem + solve surface)."""
 
-    def __init__(self, cfg: ocp.OCPConfig, prob: ocp.Problem, box: bool = True, consts: Consts | None = None):
-        self.cfg, self.prob, self.box = cfg, prob, box
+    def __init__(self, cfg_or_model, prob: ocp.Problem | None = None, box: bool = True, consts: Consts | None = None):
+        """SolverBoxFDDP(problem): either (OCPConfig, Problem) for the reference
+        OCP, or a model object with running()/terminal()/x0/N/nx/nu/u_lb/u_ub."""
+        model = ocp.RobotOCP(cfg_or_model, prob) if prob is not None else cfg_or_model
+        self.model, self.box = model, box
+        self.cfg, self.prob = getattr(model, "cfg", None), getattr(model, "prob", None)
         self.c = consts or Consts()
         self.th_stop = self.c.th_stop_box if box else self.c.th_stop_fddp
-        N, nx, nu = cfg.horizon, cfg.nx, 7
+        N, nx, nu = model.N, model.nx, model.nu
         self.N, self.nx, self.nu = N, nx, nu
-        self.u_lb = -np.asarray(cfg.tau_limits, float)
-        self.u_ub = np.asarray(cfg.tau_limits, float)
+        self.x0 = np.asarray(model.x0, float)
+        self.u_lb = np.asarray(model.u_lb, float)
+        self.u_ub = np.asarray(model.u_ub, float)
         self.k = np.zeros((N, nu))
         self.K = np.zeros((N, nu, nx))
         self.stats = Stats()
 
     # --- problem evaluations -------------------------------------------------
     def _calc_diff(self):
-        cfg, prob, N = self.cfg, self.prob, self.N
-        run = ocp.running_eval(cfg, prob, slice(0, N), self.xs[:N], self.us, True)
-        term = ocp.terminal_eval(cfg, prob, self.xs[N], True)
+        N = self.N
+        run = self.model.running(slice(0, N), self.xs[:N], self.us, True)
+        term = self.model.terminal(self.xs[N], True)
         self.run, self.term = run, term
         self.cost = float(np.sum(run["cost"]) + term["cost"])  # ShootingProblem::calcDiff sum
         self.fs = np.zeros((N + 1, self.nx))
         if not self.is_feasible:
-            self.fs[0] = prob.x0 - self.xs[0]
+            self.fs[0] = self.x0 - self.xs[0]
             self.fs[1:] = run["xnext"] - self.xs[1:]
 
     def _backward(self):
@@ -230,11 +235,11 @@ class SolverBoxFDDP:
         return self.dg + dv, self.dq - 2.0 * dv
 
     def _forward(self, alpha):
-        cfg, prob, N = self.cfg, self.prob, self.N
+        N = self.N
         xs_try = np.zeros_like(self.xs)
         us_try = np.zeros_like(self.us)
         cost_try = 0.0
-        xnext = prob.x0.copy()
+        xnext = self.x0.copy()
         gap = not (self.is_feasible or alpha == 1.0)
         for t in range(N):
             xs_try[t] = xnext + self.fs[t] * (alpha - 1.0) if gap else xnext
@@ -243,13 +248,13 @@ class SolverBoxFDDP:
             if self.box:
                 u = np.minimum(np.maximum(u, self.u_lb), self.u_ub)
             us_try[t] = u
-            d = ocp.running_eval(cfg, prob, t, xs_try[t], us_try[t], False)
+            d = self.model.running(t, xs_try[t], us_try[t], False)
             xnext = d["xnext"]
             cost_try += float(d["cost"])
             if raise_if_nan(cost_try) or raise_if_nan(float(np.max(np.abs(xnext)))):
                 raise ForwardError("nan")
         xs_try[N] = xnext + self.fs[N] * (alpha - 1.0) if gap else xnext
-        d = ocp.terminal_eval(cfg, prob, xs_try[N], False)
+        d = self.model.terminal(xs_try[N], False)
         cost_try += float(d["cost"])
         if raise_if_nan(cost_try):
             raise ForwardError("nan")
@@ -305,7 +310,11 @@ class SolverBoxFDDP:
                 if dVexp >= 0:
                     ok = abs(d0) < c.th_grad or dV > c.th_acceptstep * dVexp
                 else:
-                    ok = abs(d0) < c.th_grad or dV < c.th_acceptnegstep * dVexp
+                    # gap-closing branch: accept a cost increase of up to
+                    # th_acceptnegstep x the predicted one.  (SURVEY.md B.1 writes
+                    # "dV < 2 dVexp"; that rejects the exact LQR step — see
+                    # tests/test_oracle.py::test_fddp_lqr_known_answer.)
+                    ok = abs(d0) < c.th_grad or dV > c.th_acceptnegstep * dVexp
                 if ok:
                     self.was_feasible = self.is_feasible
                     self.xs, self.us = xs_try, us_try
@@ -327,5 +336,5 @@ class SolverBoxFDDP:
 
     def contact_force(self, t: int):
         """lambda at knot t evaluated at the final (xs, us) (fn_pred source, R7)."""
-        d = ocp.running_eval(self.cfg, self.prob, t, self.xs[t], self.us[t], False)
+        d = self.model.running(t, self.xs[t], self.us[t], False)
         return d["lam"]

@@ -463,22 +463,18 @@ def _ff_soft(cfg, w):
     return cost, grad, active.astype(float)
 
 
-def ff_eval(cfg, refs, y, w, surface, terminal, diff):
-    """_AugmentedLPFActionModel.calc / calcDiff (crocoddyl_force_feedback.py:211-290).
-
-    Terminal nodes are called by the solver without u -> w = 0 and the inner
-    IAM is evaluated with running semantics at u = tau (R1)."""
+def ff_augment(cfg, inner, y, w, yref, diff):
+    """Augmentation algebra of _AugmentedLPFActionModel.calc / calcDiff
+    (crocoddyl_force_feedback.py:211-290) given the inner IAM results
+    `inner` (xnext, cost and, if diff, Fx, Fu, Lx, Lu, Lxx, Lxu, Luu)."""
     alpha = float(np.clip(cfg.ff_alpha, 0.0, 0.999999))
     beta = 1.0 - alpha
-    x_mb, tau = y[..., :14], y[..., 14:21]
-    if terminal:
-        w = np.zeros_like(tau)
-    inner = iam_eval(cfg, refs, x_mb, tau, surface, "terminal_u" if terminal else "running", diff)
-    out = dict(lam=inner["lam"])
+    tau = y[..., 14:21]
+    out = dict(lam=inner.get("lam"))
     out["xnext"] = np.concatenate([inner["xnext"], alpha * tau + beta * w], -1)
     cost = inner["cost"]
     Wy2 = np.square(np.asarray(cfg.y_weights, float))
-    dy = y - refs["y_ref"]
+    dy = y - yref
     w_y = max(cfg.w_y, 0.0)
     w_w = max(cfg.w_w, 0.0)
     w_s = max(cfg.w_w_soft_limits, 0.0)
@@ -519,6 +515,17 @@ def ff_eval(cfg, refs, y, w, surface, terminal, diff):
     return out
 
 
+def ff_eval(cfg, refs, y, w, surface, terminal, diff):
+    """_AugmentedLPFActionModel around the inner IAM.  Terminal nodes are
+    called by the solver without u -> w = 0 and the inner IAM is evaluated
+    with running semantics at u = tau (R1)."""
+    tau = y[..., 14:21]
+    if terminal:
+        w = np.zeros_like(tau)
+    inner = iam_eval(cfg, refs, y[..., :14], tau, surface, "terminal_u" if terminal else "running", diff)
+    return ff_augment(cfg, inner, y, w, refs["y_ref"], diff)
+
+
 def node_refs(prob: Problem, idx):
     return dict(
         p_ref=prob.p_ref[idx],
@@ -542,3 +549,54 @@ def terminal_eval(cfg, prob, x, diff):
     if cfg.variant == "ff":
         return ff_eval(cfg, refs, x, None, prob.surface, True, diff)
     return iam_eval(cfg, refs, x, None, prob.surface, "terminal_x", diff)
+
+
+class RobotOCP:
+    """The reference's ShootingProblem for one instance, as the solver sees it."""
+
+    def __init__(self, cfg: OCPConfig, prob: Problem):
+        self.cfg, self.prob = cfg, prob
+        self.N, self.nx, self.nu = cfg.horizon, cfg.nx, 7
+        self.x0 = prob.x0
+        self.u_lb = -np.asarray(cfg.tau_limits, float)
+        self.u_ub = np.asarray(cfg.tau_limits, float)
+
+    def running(self, idx, x, u, diff):
+        return running_eval(self.cfg, self.prob, idx, x, u, diff)
+
+    def terminal(self, x, diff):
+        return terminal_eval(self.cfg, self.prob, x, diff)
+
+
+class LQRProblem:
+    """Linear dynamics x+ = A x + B u + c, cost 0.5 x'Qx + q'x + 0.5 u'Ru + r'u per
+    running node (terminal: Qf, qf) — a known-answer model for the solver."""
+
+    def __init__(self, A, B, c, Q, q, R, r, Qf, qf, x0, N, u_lb=None, u_ub=None):
+        self.A, self.B, self.c, self.Q, self.q, self.R, self.r, self.Qf, self.qf = A, B, c, Q, q, R, r, Qf, qf
+        self.x0, self.N = np.asarray(x0, float), int(N)
+        self.nx, self.nu = A.shape[0], B.shape[1]
+        inf = np.full(self.nu, np.inf)
+        self.u_lb = -inf if u_lb is None else np.asarray(u_lb, float)
+        self.u_ub = inf if u_ub is None else np.asarray(u_ub, float)
+
+    def running(self, idx, x, u, diff):
+        xn = x @ self.A.T + u @ self.B.T + self.c
+        cost = 0.5 * np.einsum("...i,ij,...j->...", x, self.Q, x) + x @ self.q
+        cost = cost + 0.5 * np.einsum("...i,ij,...j->...", u, self.R, u) + u @ self.r
+        out = dict(xnext=xn, cost=cost, lam=None)
+        if diff:
+            b = x.shape[:-1]
+            out.update(
+                Fx=np.broadcast_to(self.A, b + self.A.shape).copy(), Fu=np.broadcast_to(self.B, b + self.B.shape).copy(),
+                Lx=x @ self.Q + self.q, Lu=u @ self.R + self.r,
+                Lxx=np.broadcast_to(self.Q, b + self.Q.shape).copy(), Luu=np.broadcast_to(self.R, b + self.R.shape).copy(),
+                Lxu=np.zeros(b + (self.nx, self.nu)),
+            )
+        return out
+
+    def terminal(self, x, diff):
+        out = dict(xnext=x.copy(), cost=0.5 * x @ self.Qf @ x + self.qf @ x, lam=None)
+        if diff:
+            out.update(Lx=self.Qf @ x + self.qf, Lxx=self.Qf.copy())
+        return out

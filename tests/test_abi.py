@@ -1,0 +1,84 @@
+"""C-ABI: library loads on a CPU-only host, exports every declared symbol,
+struct layouts agree with the header, host helpers agree with the oracle,
+and API errors are reported (no compute on the device here)."""
+import ctypes
+import re
+import subprocess
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+from ffddp import _abi
+from oracle import panda as P
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "ffddp.h"
+
+
+def declared_functions():
+    txt = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(ffddp_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.load()
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_abi.SYMBOLS)
+
+
+def test_struct_layout_matches_header():
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "ffddp.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(ffddp_robot), sizeof(ffddp_ocp_config),
+         offsetof(ffddp_ocp_config, dt), offsetof(ffddp_ocp_config, R_des),
+         offsetof(ffddp_ocp_config, y_weights), offsetof(ffddp_ocp_config, use_inner_tau_reg));
+  return 0;
+}'''
+    with tempfile.TemporaryDirectory() as d:
+        c = Path(d) / "t.c"
+        c.write_text(src)
+        exe = Path(d) / "t"
+        subprocess.run(["gcc", "-I", str(ROOT / "include"), str(c), "-o", str(exe)], check=True)
+        vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    C = _abi.OcpConfig
+    assert vals == [
+        ctypes.sizeof(_abi.Robot), ctypes.sizeof(C), C.dt.offset, C.R_des.offset, C.y_weights.offset,
+        C.use_inner_tau_reg.offset,
+    ]
+
+
+def test_host_helpers_match_oracle():
+    rng = np.random.default_rng(0)
+    q = P.Q_NEUTRAL + rng.uniform(-0.5, 0.5, size=(16, 7))
+    assert np.allclose(_abi.gravity_torque(q), P.gravity_torque(q), rtol=0, atol=1e-12)
+    for i in range(4):
+        Rm, p = _abi.frame_placement(q[i])
+        _, _, R2, p2 = P.forward_kinematics(q[i])
+        assert np.allclose(Rm, R2, atol=1e-14) and np.allclose(p, p2, atol=1e-14)
+
+
+def test_invalid_config_rejected_before_device():
+    from ffddp.config import classical_preset
+
+    lib = _abi.load()
+    c = classical_preset(30).to_struct()
+    c.nc = 2  # neither ContactModel1D nor 3D
+    h = ctypes.c_void_p()
+    rc = lib.ffddp_create(ctypes.byref(_abi.robot_struct()), ctypes.byref(c), 0, 4, ctypes.byref(h))
+    assert rc == -1 and not h.value
+    c = classical_preset(30).to_struct()
+    rc = lib.ffddp_create(ctypes.byref(_abi.robot_struct()), ctypes.byref(c), 0, 0, ctypes.byref(h))
+    assert rc == -1
+
+
+def test_null_handle_errors():
+    lib = _abi.load()
+    assert lib.ffddp_profile_enable(None, 1) == -1
+    assert b"null" in lib.ffddp_last_error(None)
