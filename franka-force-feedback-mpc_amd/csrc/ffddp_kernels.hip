@@ -290,31 +290,19 @@ __global__ __launch_bounds__(NODE_BLOCK) void k_node(const DevConsts* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// backward pass: one wavefront per instance
+// backward pass (SolverDDP::backwardPass + SolverBoxFDDP::computeGains)
+//
+// Column-per-lane layout: a group of G lanes (G = 16 for nx = 14, 32 for
+// nx = 21) owns one instance; lane j keeps column j of V_xx in registers and
+// computes column j of T1 = Fx^T V_xx', Q_xx, K and the new V_xx.  Fx / Fu are
+// never materialised: with the Euler structure
+//   Fx = I + [[dt^2 A_x],[dt A_x]] + [[0, dt I],[0, 0]],  Fu = [[dt^2 A_u],[dt A_u]]
+// (FF: extra rows [0, alpha I] / [beta I]) every product is a 7-deep
+// contraction with the node's acceleration Jacobian A (half the flops of the
+// dense 14x14x14 products).  One wavefront = 64/G instances; the serial gains
+// (LLT or BoxQP) of those instances run concurrently on their group leaders.
 // ---------------------------------------------------------------------------
 constexpr int NXM = 21;
-
-struct BwShared {
-  double Vxx[NXM * NXM];
-  double Vx[NXM];
-  double Fx[NXM * NXM];
-  double Fu[NXM * NU];
-  double T1[NXM * NXM];  // Fx^T Vxx'
-  double T2[NU * NXM];   // Fu^T Vxx'
-  double Qxx[NXM * NXM];
-  double Qxu[NXM * NU];
-  double Quu[NU * NU];
-  double Qx[NXM];
-  double Qu[NU];
-  double Qinv[NU * NU];  // Quu^-1 restricted to the free set (BoxQP) / unused for LLT
-  double L[28];
-  double K[NU * NXM];
-  double kk[NU];
-  double fs[NXM];
-  double red[64];
-  int flag;
-  int clamped[NU];
-};
 
 __device__ __forceinline__ bool bad(double v) { return isnan(v) || isinf(v) || v >= 1e30; }
 
@@ -419,154 +407,206 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+template <int G> __device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+template <int G> __device__ __forceinline__ int group_or(int v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+  return v;
+}
+
+template <bool FF> struct BwGroup {
+  static constexpr int NX = FF ? 21 : 14;
+  double A[21 * 7];  // A[dir][comp]
+  double T1[NX * NX];
+  double Z[NX * 7];  // Z[i][m] = dt^2 T1[i][m] + dt T1[i][m+7]
+  double Qxx[NX * NX];
+  double Qxu[NX * 7];
+  double T2[7 * NX];
+  double Quu[49];
+  double L[28];
+  double K[7 * NX];  // K[c][j]
+  double Qu[7], kk[7], fs[NX], Vx[NX];
+  int flag;
+  int clamped[7];
+};
+
 template <bool FF>
 __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restrict__ Cg, Dev d, int iter) {
+  constexpr int NX = FF ? 21 : 14;
+  constexpr int G = FF ? 32 : 16;
+  constexpr int IPB = BW_BLOCK / G;
   const DevConsts& C = *Cg;
   const int N = C.N;
-  constexpr int nx = FF ? 21 : 14;
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  if (b >= d.B) return;
-  InstState* st = d.st + b;
-  if (st->done) return;
-  __shared__ BwShared S;
-  constexpr bool ff = FF;
-  const double dt = C.dt;
-  const bool feas = st->is_feasible != 0;
-  const bool use_qp = C.use_box && feas;
-  const double* recb = d.rec_buf + (long)b * (N + 1) * d.rec;
-  // total cost from the fresh calc (ShootingProblem::calcDiff sum, t = 0..N)
-  if (st->recalc && tid == 0) {
-    st->n_calc += 1;
-    double c = 0.0;
-    for (int t = 0; t <= N; ++t) c += recb[(long)t * d.rec + rec_off_cost(nx)];
-    st->cost = c;
+  __shared__ BwGroup<FF> SS[IPB];
+  const int grp = threadIdx.x / G, j = threadIdx.x % G;
+  const int b = blockIdx.x * IPB + grp;
+  BwGroup<FF>& S = SS[grp];
+  bool finished = true;
+  InstState* st = nullptr;
+  if (b < d.B) {
+    st = d.st + b;
+    finished = st->done != 0;
   }
-  double preg = st->preg;
+  const bool active = !finished;
+  const bool feas = active ? st->is_feasible != 0 : true;
+  const bool use_qp = C.use_box && feas;
+  const double dt = C.dt, dt2 = C.dt * C.dt;
+  const double* recb = d.rec_buf + (long)(active ? b : 0) * (N + 1) * d.rec;
+  const int rec = d.rec;
+  if (active && j == 0 && st->recalc) {
+    // ShootingProblem::calcDiff cost, summed over t = 0..N
+    double c = 0.0;
+    for (int t = 0; t <= N; ++t) c += recb[(long)t * rec + rec_off_cost(NX)];
+    st->cost = c;
+    st->n_calc += 1;
+  }
+  double preg = active ? st->preg : 0.0;
   int retries = 0;
+  bool fail_inst = false;
+  double dg = 0.0, dq = 0.0, stop = 0.0;
   for (;;) {
-    __syncthreads();
-    if (tid == 0) S.flag = 0;
-    // terminal: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N)
-    const double* rT = recb + (long)N * d.rec;
-    const double* fsN = d.fs + ((long)b * (N + 1) + N) * nx;
-    for (int e = tid; e < nx * nx; e += BW_BLOCK) {
-      const int i = e / nx, j = e % nx;
-      S.Vxx[e] = rT[rec_off_Lxx(nx) + e] + (i == j ? preg : 0.0);
-    }
-    for (int i = tid; i < nx; i += BW_BLOCK) S.fs[i] = fsN[i];
-    __syncthreads();
-    double dg = 0.0, dq = 0.0, stop = 0.0;  // lane-0 accumulators
-    for (int i = tid; i < nx; i += BW_BLOCK) {
-      double acc = rT[rec_off_Lx(nx) + i];
-      if (!feas)
-        for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
-      S.Vx[i] = acc;
-    }
-    __syncthreads();
-    // gap terms of the terminal node and w_N = Vxx_N fs_N
-    if (!feas) {
-      double* wN = d.w + ((long)b * (N + 1) + N) * nx;
-      for (int i = tid; i < nx; i += BW_BLOCK) {
-        double acc = 0.0;
-        for (int j = 0; j < nx; ++j) acc += S.Vxx[i * nx + j] * S.fs[j];
-        wN[i] = acc;
-      }
-      double c1 = 0.0, c2 = 0.0;
-      if (tid < nx) {
-        double acc = 0.0;
-        for (int j = 0; j < nx; ++j) acc += S.Vxx[tid * nx + j] * S.fs[j];
-        c1 = S.Vx[tid] * S.fs[tid];
-        c2 = S.fs[tid] * acc;
-      }
-      dg -= wave_sum(c1);
-      dq += wave_sum(c2);
-    }
     bool failed = false;
+    const bool work0 = !finished;
+    dg = dq = stop = 0.0;
+    double Vcol[NX];
+    double vx_j = 0.0;
+    // ---- terminal node: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N) ----
+    if (work0 && j < NX) {
+      const double* rT = recb + (long)N * rec;
+      const double* fsN = d.fs + ((long)b * (N + 1) + N) * NX;
+      double vfs = 0.0;
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        Vcol[i] = rT[rec_off_Lxx(NX) + i * NX + j] + (i == j ? preg : 0.0);
+        vfs += Vcol[i] * fsN[i];
+      }
+      const double fj = fsN[j];
+      vx_j = rT[rec_off_Lx(NX) + j] + (feas ? 0.0 : vfs);
+      if (!feas) {
+        d.w[((long)b * (N + 1) + N) * NX + j] = vfs;
+        dg -= vx_j * fj;
+        dq += fj * vfs;
+      }
+      S.Vx[j] = vx_j;
+    }
+    __syncthreads();
     for (int t = N - 1; t >= 0; --t) {
-      const double* r = recb + (long)t * d.rec;
-      const double* A = r + rec_off_A();
+      const bool work = work0 && !failed;
+      const double* r = recb + (long)t * rec;
+      if (work) {
+        for (int e = j; e < 147; e += G) S.A[e] = r[rec_off_A() + e];
+        if (j < NX) S.fs[j] = d.fs[((long)b * (N + 1) + t) * NX + j];
+      }
       __syncthreads();
-      // Fx, Fu from the node's acceleration Jacobian (IntegratedActionModelEuler::calcDiff)
-      for (int e = tid; e < nx * nx; e += BW_BLOCK) {
-        const int i = e / nx, j = e % nx;
-        double v = (i == j) ? 1.0 : 0.0;
-        if (i < 14 && j < (ff ? 21 : 14)) {
-          const double aij = A[j * NQ + (i % 7)];
-          v += (i < 7 ? dt * dt : dt) * aij;
-          if (i < 7 && j == i + 7) v += dt;
+      double Arow[7];
+      if (work && j < NX) {
+        // ---- T1 = Fx^T Vxx' (column j), T2 = Fu^T Vxx' (column j), Qx ----
+        double W[7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) W[m] = dt2 * Vcol[m] + dt * Vcol[m + 7];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          double acc = (i < 14) ? Vcol[i] : C.alpha * Vcol[i];
+          if (i >= 7 && i < 14) acc += dt * Vcol[i - 7];
+#pragma unroll
+          for (int m = 0; m < 7; ++m) acc += S.A[i * 7 + m] * W[m];
+          S.T1[i * NX + j] = acc;
         }
-        if (ff && i >= 14) v = (i == j) ? C.alpha : 0.0;
-        S.Fx[e] = v;
-      }
-      for (int e = tid; e < nx * NU; e += BW_BLOCK) {
-        const int i = e / NU, kk = e % NU;
-        double v;
-        if (!ff)
-          v = (i < 7 ? dt * dt : dt) * A[(14 + kk) * NQ + (i % 7)];
-        else
-          v = (i >= 14 && i - 14 == kk) ? C.beta : 0.0;
-        S.Fu[e] = v;
-      }
-      const double* fst = d.fs + ((long)b * (N + 1) + t) * nx;
-      for (int i = tid; i < nx; i += BW_BLOCK) S.fs[i] = fst[i];
-      __syncthreads();
-      // T1 = Fx^T Vxx', T2 = Fu^T Vxx', Qx, Qu
-      for (int e = tid; e < nx * nx; e += BW_BLOCK) {
-        const int i = e / nx, j = e % nx;
-        double acc = 0.0;
-        for (int k = 0; k < nx; ++k) acc += S.Fx[k * nx + i] * S.Vxx[k * nx + j];
-        S.T1[e] = acc;
-      }
-      for (int e = tid; e < NU * nx; e += BW_BLOCK) {
-        const int i = e / nx, j = e % nx;
-        double acc = 0.0;
-        for (int k = 0; k < nx; ++k) acc += S.Fu[k * NU + i] * S.Vxx[k * nx + j];
-        S.T2[e] = acc;
-      }
-      if (tid < nx) {
-        double acc = r[rec_off_Lx(nx) + tid];
-        for (int k = 0; k < nx; ++k) acc += S.Fx[k * nx + tid] * S.Vx[k];
-        S.Qx[tid] = acc;
-      } else if (tid >= 32 && tid < 32 + NU) {
-        const int i = tid - 32;
-        double acc = r[rec_off_Lu(nx) + i];
-        for (int k = 0; k < nx; ++k) acc += S.Fu[k * NU + i] * S.Vx[k];
-        S.Qu[i] = acc;
+#pragma unroll
+        for (int c = 0; c < 7; ++c) {
+          double acc;
+          if (FF) {
+            acc = C.beta * Vcol[14 + c];
+          } else {
+            acc = 0.0;
+#pragma unroll
+            for (int m = 0; m < 7; ++m) acc += S.A[(14 + c) * 7 + m] * W[m];
+          }
+          S.T2[c * NX + j] = acc;
+        }
+#pragma unroll
+        for (int m = 0; m < 7; ++m) Arow[m] = S.A[j * 7 + m];
       }
       __syncthreads();
-      for (int e = tid; e < nx * nx; e += BW_BLOCK) {
-        const int i = e / nx, j = e % nx;
-        double acc = r[rec_off_Lxx(nx) + e];
-        for (int k = 0; k < nx; ++k) acc += S.T1[i * nx + k] * S.Fx[k * nx + j];
-        S.Qxx[e] = acc;
-      }
-      for (int e = tid; e < nx * NU; e += BW_BLOCK) {
-        const int i = e / NU, j = e % NU;
-        double acc = r[rec_off_Lxu(nx) + e];
-        for (int k = 0; k < nx; ++k) acc += S.T1[i * nx + k] * S.Fu[k * NU + j];
-        S.Qxu[e] = acc;
-      }
-      if (tid < NU * NU) {
-        const int i = tid / NU, j = tid % NU;
-        double acc = r[rec_off_Luu(nx) + tid];
-        for (int k = 0; k < nx; ++k) acc += S.T2[i * nx + k] * S.Fu[k * NU + j];
-        if (i == j) acc += preg;
-        S.Quu[tid] = acc;
+      double qx_j = 0.0;
+      if (work && j < NX) {
+        double wv[7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) wv[m] = dt2 * S.Vx[m] + dt * S.Vx[m + 7];
+        qx_j = r[rec_off_Lx(NX) + j] + ((j < 14) ? S.Vx[j] : C.alpha * S.Vx[j]);
+        if (j >= 7 && j < 14) qx_j += dt * S.Vx[j - 7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) qx_j += Arow[m] * wv[m];
+        if (j < 7) {
+          double qu = r[rec_off_Lu(NX) + j];
+          if (FF) {
+            qu += C.beta * S.Vx[14 + j];
+          } else {
+#pragma unroll
+            for (int m = 0; m < 7; ++m) qu += S.A[(14 + j) * 7 + m] * wv[m];
+          }
+          S.Qu[j] = qu;
+        }
+        // Z row j
+#pragma unroll
+        for (int m = 0; m < 7; ++m) S.Z[j * 7 + m] = dt2 * S.T1[j * NX + m] + dt * S.T1[j * NX + m + 7];
       }
       __syncthreads();
-      // gains (one lane, registers)
-      if (tid == 0) {
+      if (work && j < NX) {
+        // ---- Qxx column j = Lxx + T1 Fx ; Qxu row j = Lxu + T1 Fu ; Quu column j ----
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          double acc = r[rec_off_Lxx(NX) + i * NX + j];
+          acc += (j < 14) ? S.T1[i * NX + j] : C.alpha * S.T1[i * NX + j];
+          if (j >= 7 && j < 14) acc += dt * S.T1[i * NX + j - 7];
+#pragma unroll
+          for (int m = 0; m < 7; ++m) acc += S.Z[i * 7 + m] * Arow[m];
+          S.Qxx[i * NX + j] = acc;
+        }
+#pragma unroll
+        for (int c = 0; c < 7; ++c) {
+          double acc = r[rec_off_Lxu(NX) + j * 7 + c];
+          if (FF) {
+            acc += C.beta * S.T1[j * NX + 14 + c];
+          } else {
+#pragma unroll
+            for (int m = 0; m < 7; ++m) acc += S.Z[j * 7 + m] * S.A[(14 + c) * 7 + m];
+          }
+          S.Qxu[j * 7 + c] = acc;
+        }
+        if (j < 7) {
+#pragma unroll
+          for (int c = 0; c < 7; ++c) {
+            double acc = r[rec_off_Luu(NX) + c * 7 + j];
+            if (FF) {
+              acc += C.beta * S.T2[c * NX + 14 + j];
+            } else {
+#pragma unroll
+              for (int m = 0; m < 7; ++m)
+                acc += (dt2 * S.T2[c * NX + m] + dt * S.T2[c * NX + m + 7]) * S.A[(14 + j) * 7 + m];
+            }
+            if (c == j) acc += preg;
+            S.Quu[c * 7 + j] = acc;
+          }
+        }
+      }
+      __syncthreads();
+      // ---- gains: Eigen::LLT (infeasible) or BoxQP (feasible, bounded) ----
+      if (work && j == 0) {
         double H[NU * NU];
 #pragma unroll
         for (int e = 0; e < NU * NU; ++e) H[e] = S.Quu[e];
-        bool ok = true;
+        bool ok;
         if (!use_qp) {
           double L[28];
 #pragma unroll
           for (int i = 0; i < NU; ++i)
 #pragma unroll
-            for (int j = 0; j <= i; ++j) L[tri(i, j)] = H[i * NU + j];
+            for (int jj = 0; jj <= i; ++jj) L[tri(i, jj)] = H[i * NU + jj];
           ok = chol_packed<NU>(L);
 #pragma unroll
           for (int e = 0; e < 28; ++e) S.L[e] = L[e];
@@ -591,130 +631,126 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
           for (int i = 0; i < NU; ++i) {
             S.kk[i] = -x[i];
             S.clamped[i] = cl[i] ? 1 : 0;
+            if (cl[i]) S.Qu[i] = 0.0;  // BoxFDDP: clamped Qu entries are zeroed
           }
         }
         S.flag = ok ? 0 : 1;
       }
       __syncthreads();
-      if (S.flag) {
-        failed = true;
-        break;
-      }
-      // K = Quu^-1 Qxu^T, one rhs per lane (BoxQP: masked solve on the free set,
-      // i.e. Quu_inv restricted to the free block); LLT path: k = Quu^-1 Qu
-      if (tid < nx || (!use_qp && tid == nx)) {
-        double rhs[NU];
-        if (tid < nx) {
+      if (work && S.flag) failed = true;
+      const bool work2 = work && !failed;
+      double Kcol[7];
+      if (work2 && (j < NX || (!use_qp && j == NX))) {
+        if (j < NX) {
 #pragma unroll
-          for (int i = 0; i < NU; ++i) rhs[i] = S.clamped[i] ? 0.0 : S.Qxu[tid * NU + i];
+          for (int c = 0; c < 7; ++c) Kcol[c] = S.clamped[c] ? 0.0 : S.Qxu[j * 7 + c];
         } else {
 #pragma unroll
-          for (int i = 0; i < NU; ++i) rhs[i] = S.Qu[i];
+          for (int c = 0; c < 7; ++c) Kcol[c] = S.Qu[c];
         }
-        chol_solve<NU>(S.L, rhs);
-        if (tid < nx) {
+        chol_solve<NU>(S.L, Kcol);
+        if (j < NX) {
 #pragma unroll
-          for (int i = 0; i < NU; ++i) S.K[i * nx + tid] = rhs[i];
+          for (int c = 0; c < 7; ++c) S.K[c * NX + j] = Kcol[c];
         } else {
 #pragma unroll
-          for (int i = 0; i < NU; ++i) S.kk[i] = rhs[i];
+          for (int c = 0; c < 7; ++c) S.kk[c] = Kcol[c];
         }
       }
       __syncthreads();
-      if (use_qp && tid == 0)
-        for (int i = 0; i < NU; ++i)
-          if (S.clamped[i]) S.Qu[i] = 0.0;
-      __syncthreads();
-      // Vx = Qx - K^T Qu ; Vxx = sym(Qxx - Qxu K) + preg I ; Vx += Vxx fs
-      for (int e = tid; e < nx * nx; e += BW_BLOCK) {
-        const int i = e / nx, j = e % nx;
-        double a1 = S.Qxx[i * nx + j], a2 = S.Qxx[j * nx + i];
-        for (int m = 0; m < NU; ++m) {
-          a1 -= S.Qxu[i * NU + m] * S.K[m * nx + j];
-          a2 -= S.Qxu[j * NU + m] * S.K[m * nx + i];
+      int badv = 0;
+      double c_dg = 0.0, c_dq = 0.0, c_st = 0.0;
+      if (work2 && j < NX) {
+        // ---- Vxx = sym(Qxx - Qxu K) + preg I (column j) ; Vx = Qx - K^T Qu (+ Vxx fs) ----
+        double qxu_j[7];
+#pragma unroll
+        for (int c = 0; c < 7; ++c) qxu_j[c] = S.Qxu[j * 7 + c];
+        double vfs = 0.0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          double a1 = S.Qxx[i * NX + j], a2 = S.Qxx[j * NX + i];
+#pragma unroll
+          for (int c = 0; c < 7; ++c) {
+            a1 -= S.Qxu[i * 7 + c] * Kcol[c];
+            a2 -= qxu_j[c] * S.K[c * NX + i];
+          }
+          const double v = 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
+          Vcol[i] = v;
+          vfs += v * S.fs[i];
+          badv |= bad(fabs(v)) ? 1 : 0;
         }
-        S.T1[e] = 0.5 * (a1 + a2) + (i == j ? preg : 0.0);  // new Vxx staged in T1
-      }
-      __syncthreads();
-      for (int e = tid; e < nx * nx; e += BW_BLOCK) S.Vxx[e] = S.T1[e];
-      __syncthreads();
-      double wt = 0.0;
-      if (tid < nx) {
-        double acc = S.Qx[tid];
-        for (int m = 0; m < NU; ++m) acc -= S.K[m * nx + tid] * S.Qu[m];
-        double vf = 0.0;
-        for (int j = 0; j < nx; ++j) vf += S.Vxx[tid * nx + j] * S.fs[j];
-        wt = vf;
-        if (!feas) acc += vf;
-        S.Vx[tid] = acc;
-      }
-      __syncthreads();
-      // NaN / inf checks, store gains and w_t = Vxx_t fs_t
-      {
-        bool badv = false;
-        for (int e = tid; e < nx * nx; e += BW_BLOCK) badv |= bad(fabs(S.Vxx[e]));
-        if (tid < nx) badv |= bad(fabs(S.Vx[tid]));
-        if (badv) S.flag = 1;
-      }
-      double* Kt = d.K + ((long)b * N + t) * NU * nx;
-      for (int e = tid; e < NU * nx; e += BW_BLOCK) Kt[e] = S.K[e];
-      if (tid < NU) d.k[((long)b * N + t) * NU + tid] = S.kk[tid];
-      if (tid < nx && !feas) d.w[((long)b * (N + 1) + t) * nx + tid] = wt;
-      __syncthreads();
-      if (S.flag) {
-        failed = true;
-        break;
-      }
-      {
-        // expected-improvement partials (SolverFDDP::updateExpectedImprovement), wave-reduced
-        double c_dg = 0.0, c_dq = 0.0, c_st = 0.0;
-        if (tid < NU) {
+        double vx = qx_j;
+#pragma unroll
+        for (int c = 0; c < 7; ++c) vx -= Kcol[c] * S.Qu[c];
+        if (!feas) vx += vfs;
+        badv |= bad(fabs(vx)) ? 1 : 0;
+        vx_j = vx;
+        double* Kt = d.K + ((long)b * N + t) * NU * NX;
+#pragma unroll
+        for (int c = 0; c < 7; ++c) Kt[c * NX + j] = Kcol[c];
+        if (!feas) {
+          d.w[((long)b * (N + 1) + t) * NX + j] = vfs;
+          c_dg -= vx * S.fs[j];
+          c_dq += S.fs[j] * vfs;
+        }
+        if (j < 7) {
           double quk = 0.0;
 #pragma unroll
-          for (int j = 0; j < NU; ++j) quk += S.Quu[tid * NU + j] * S.kk[j];
-          c_dg += S.Qu[tid] * S.kk[tid];
-          c_dq -= S.kk[tid] * quk;
-          c_st += S.Qu[tid] * S.Qu[tid];
+          for (int m = 0; m < 7; ++m) quk += S.Quu[j * 7 + m] * S.kk[m];
+          c_dg += S.Qu[j] * S.kk[j];
+          c_dq -= S.kk[j] * quk;
+          c_st += S.Qu[j] * S.Qu[j];
+          d.k[((long)b * N + t) * NU + j] = S.kk[j];
         }
-        if (!feas && tid < nx) {
-          c_dg -= S.Vx[tid] * S.fs[tid];
-          c_dq += S.fs[tid] * wt;
+      }
+      badv = group_or<G>(badv);
+      c_dg = group_sum<G>(c_dg);
+      c_dq = group_sum<G>(c_dq);
+      c_st = group_sum<G>(c_st);
+      __syncthreads();
+      if (work2) {
+        if (badv) {
+          failed = true;
+        } else {
+          dg += c_dg;
+          dq += c_dq;
+          stop += c_st;
+          if (j < NX) S.Vx[j] = vx_j;
         }
-        c_dg = wave_sum(c_dg);
-        c_dq = wave_sum(c_dq);
-        c_st = wave_sum(c_st);
-        dg += c_dg;
-        dq += c_dq;
-        stop += c_st;
+      }
+      __syncthreads();
+    }
+    // ---- retry bookkeeping (SolverFDDP::solve: increaseRegularization) ----
+    if (!finished) {
+      if (failed) {
+        retries++;
+        preg = fmin(preg * C.reg_inc, C.reg_max);
+        if (preg == C.reg_max) {
+          finished = true;
+          fail_inst = true;
+        }
+      } else {
+        finished = true;
       }
     }
-    if (!failed) {
-      if (tid == 0) {
-        st->dg = dg;
-        st->dq = dq;
-        st->stop = stop;
-        st->preg = preg;
-        st->bw_ok = 1;
-        st->n_retries += retries;
-        st->n_backward += retries + 1;
-        st->n_iters += 1;
-      }
-      return;
-    }
-    // SolverFDDP::solve: increaseRegularization and retry without recalcDiff
-    retries++;
-    preg = fmin(preg * C.reg_inc, C.reg_max);
-    if (preg == C.reg_max) {
-      if (tid == 0) {
-        st->preg = preg;
-        st->bw_ok = 0;
-        st->iter = iter;
-        st->done = 1;
-        st->ok = 0;
-        st->n_retries += retries;
-        st->n_backward += retries;
-      }
-      return;
+    if (__syncthreads_and(finished ? 1 : 0)) break;
+  }
+  if (active && j == 0) {
+    st->preg = preg;
+    st->n_retries += retries;
+    if (fail_inst) {
+      st->bw_ok = 0;
+      st->iter = iter;
+      st->done = 1;
+      st->ok = 0;
+      st->n_backward += retries;
+    } else {
+      st->dg = dg;
+      st->dq = dq;
+      st->stop = stop;
+      st->bw_ok = 1;
+      st->n_backward += retries + 1;
+      st->n_iters += 1;
     }
   }
 }
@@ -1145,7 +1181,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
     }
     {
       ProfScope p(h, s, KC_BACKWARD);
-      hipLaunchKernelGGL((k_backward<FF>), dim3(B), dim3(BW_BLOCK), 0, s, h->dc, d, it);
+      hipLaunchKernelGGL((k_backward<FF>), dim3((B + (FF ? 1 : 3)) / (FF ? 2 : 4)), dim3(BW_BLOCK), 0, s, h->dc, d, it);
     }
     {
       ProfScope p(h, s, KC_FORWARD);
