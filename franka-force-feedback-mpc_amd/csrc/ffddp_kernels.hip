@@ -57,6 +57,7 @@ struct Dev {
   double* trial;     // [B][T][2]  cost_try, dv
   int* trial_fail;   // [B][T]
   InstState* st;     // [B]
+  Primal* prim;      // [B][N+1]  node calc (primal) results for the calcDiff tangents
 };
 
 // ---------------------------------------------------------------------------
@@ -105,6 +106,85 @@ struct NodeShared {
   double colu[NODE_GPB][7][FFDDP_MAX_NC];  // force rows, inner-control directions
 };
 
+// calc of every node, one lane per node: the primal of calcDiff (dynamics,
+// residuals, activations, cost) plus the node cost, contact force and gap.
+template <int NC, bool FF>
+__global__ __launch_bounds__(64) void k_primal(const DevConsts* __restrict__ Cg, Dev d,
+                                               const double* __restrict__ x0,
+                                               const double* __restrict__ node_ref,
+                                               const double* __restrict__ inst_ref,
+                                               const uint8_t* __restrict__ surface, int force_all) {
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  constexpr int nx = FF ? 21 : 14;
+  const long node = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int b = (int)(node / (N + 1)), t = (int)(node % (N + 1));
+  if (b >= d.B) return;
+  if (!force_all && (d.st[b].done != 0 || d.st[b].recalc == 0)) return;
+  const bool surf = surface[b] != 0;
+  const bool terminal = t == N;
+  const int mode = !terminal ? MODE_RUNNING : (FF ? MODE_TERMINAL_U : MODE_TERMINAL_X);
+  const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
+  const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
+  const double* xreg = inst_ref + (long)b * 21;
+  const double* uin = FF ? (y + 14) : (terminal ? nullptr : d.us + ((long)b * N + t) * NU);
+  Primal P;
+  node_primal<NC>(C, mode, surf, y, uin, ref, xreg, xreg + 14, P);
+  copy_primal(P, d.prim[node]);
+  double* rec = d.rec_buf + node * d.rec;
+  // node cost (IAM scaling, FF augmentation terms)
+  double cost;
+  if (!FF) {
+    cost = terminal ? P.cost : C.dt * P.cost;
+  } else {
+    const double* ww = terminal ? nullptr : d.us + ((long)b * N + t) * NU;
+    double c = C.dt * P.cost;
+    if (C.w_y > 0.0) {
+      double a = 0.0;
+      for (int i = 0; i < 21; ++i) {
+        const double dd = y[i] - x0[(long)b * nx + i];
+        a += C.Wy2[i] * dd * dd;
+      }
+      c += 0.5 * C.w_y * a;
+    }
+    if (!terminal) {
+      if (C.w_w > 0.0) {
+        double a = 0.0;
+        for (int i = 0; i < 7; ++i) a += ww[i] * ww[i];
+        c += 0.5 * C.w_w * a;
+      }
+      if (C.w_ws > 0.0) {
+        double a = 0.0;
+        for (int i = 0; i < 7; ++i) {
+          const double ov = fabs(ww[i]) - C.ws_lim[i];
+          const double o = ov > 0.0 ? ov : 0.0;
+          a += o * o;
+        }
+        c += C.w_ws * (0.5 * a);
+      }
+    }
+    cost = c;
+  }
+  rec[rec_off_cost(nx)] = cost;
+  for (int r = 0; r < 3; ++r) rec[rec_off_lam(nx) + r] = (mode == MODE_TERMINAL_X) ? 0.0 : P.lam[r];
+  // gaps fs[t+1] = xnext_t - xs[t+1] ; fs[0] = x0 - xs[0]  (zero once feasible)
+  const bool feas = d.st[b].is_feasible != 0;
+  if (!terminal) {
+    double* f = d.fs + ((long)b * (N + 1) + t + 1) * nx;
+    const double* yn = d.xs + ((long)b * (N + 1) + t + 1) * nx;
+    for (int i = 0; i < 14; ++i) f[i] = feas ? 0.0 : P.xnext[i] - yn[i];
+    if (FF) {
+      const double* wv = d.us + ((long)b * N + t) * NU;
+      for (int i = 0; i < 7; ++i) f[14 + i] = feas ? 0.0 : (C.alpha * y[14 + i] + C.beta * wv[i]) - yn[14 + i];
+    }
+  }
+  if (t == 0) {
+    double* f = d.fs + (long)b * (N + 1) * nx;
+    for (int i = 0; i < nx; ++i) f[i] = feas ? 0.0 : x0[(long)b * nx + i] - y[i];
+  }
+}
+
+// calcDiff tangents + Gauss-Newton assembly: 16-lane group per node
 template <int NC, bool FF>
 __global__ __launch_bounds__(NODE_BLOCK) void k_node(const DevConsts* __restrict__ Cg, Dev d,
                                                       const double* __restrict__ x0,
@@ -127,12 +207,13 @@ __global__ __launch_bounds__(NODE_BLOCK) void k_node(const DevConsts* __restrict
   const int mode = !terminal ? MODE_RUNNING : (ff ? MODE_TERMINAL_U : MODE_TERMINAL_X);
   const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
   const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
-  const double* xreg = inst_ref + (long)b * 21;
-  const double* tauref = xreg + 14;
-  // inner control: classical u_t, FF tau = y[14:21]
-  const double* uin = ff ? (y + 14) : (terminal ? nullptr : d.us + ((long)b * N + t) * NU);
   Primal& P = S.P[grp];
-  if (active && lane == 0) node_primal<NC>(C, mode, surf, y, uin, ref, xreg, tauref, P);
+  if (active) {
+    const double* src = reinterpret_cast<const double*>(d.prim + node);
+    double* dst = reinterpret_cast<double*>(&P);
+    constexpr int nw = sizeof(Primal) / sizeof(double);
+    for (int e = lane; e < nw; e += NODE_GROUP) dst[e] = src[e];
+  }
   __syncthreads();
   const bool need_u = mode != MODE_TERMINAL_X;
   double da[NQ], dlam[3], col[NDENSE_MAX];
@@ -231,61 +312,6 @@ __global__ __launch_bounds__(NODE_BLOCK) void k_node(const DevConsts* __restrict
       // classical terminal: no control blocks (zero them for the calcDiff export)
       for (int i = 0; i < NQ; ++i) rec[rec_off_A() + (14 + lane) * NQ + i] = 0.0;
     }
-    if (lane == 15) {
-      // node cost, contact force, gap
-      double cost;
-      if (!ff) {
-        cost = terminal ? P.cost : C.dt * P.cost;
-      } else {
-        const double* tau = y + 14;
-        double wz[7] = {0, 0, 0, 0, 0, 0, 0};
-        const double* ww = terminal ? wz : d.us + ((long)b * N + t) * NU;
-        double c = C.dt * P.cost;
-        if (C.w_y > 0.0) {
-          double a = 0.0;
-          for (int i = 0; i < 21; ++i) {
-            const double dd = y[i] - x0[(long)b * nx + i];
-            a += C.Wy2[i] * dd * dd;
-          }
-          c += 0.5 * C.w_y * a;
-        }
-        if (C.w_w > 0.0) {
-          double a = 0.0;
-          for (int i = 0; i < 7; ++i) a += ww[i] * ww[i];
-          c += 0.5 * C.w_w * a;
-        }
-        if (C.w_ws > 0.0) {
-          double a = 0.0;
-          for (int i = 0; i < 7; ++i) {
-            const double ov = fabs(ww[i]) - C.ws_lim[i];
-            const double o = ov > 0.0 ? ov : 0.0;
-            a += o * o;
-          }
-          c += C.w_ws * (0.5 * a);
-        }
-        cost = c;
-        (void)tau;
-      }
-      rec[rec_off_cost(nx)] = cost;
-      for (int r = 0; r < 3; ++r) rec[rec_off_lam(nx) + r] = (mode == MODE_TERMINAL_X) ? 0.0 : P.lam[r];
-      // gaps fs[t+1] = xnext_t - xs[t+1] ; fs[0] = x0 - xs[0]  (zero once feasible)
-      const bool feas = d.st[b].is_feasible != 0;
-      if (!terminal) {
-        double* f = d.fs + ((long)b * (N + 1) + t + 1) * nx;
-        const double* yn = d.xs + ((long)b * (N + 1) + t + 1) * nx;
-        double xn[21];
-        for (int i = 0; i < 14; ++i) xn[i] = P.xnext[i];
-        if (ff) {
-          const double* wv = d.us + ((long)b * N + t) * NU;
-          for (int i = 0; i < 7; ++i) xn[14 + i] = C.alpha * y[14 + i] + C.beta * wv[i];
-        }
-        for (int i = 0; i < nx; ++i) f[i] = feas ? 0.0 : xn[i] - yn[i];
-      }
-      if (t == 0) {
-        double* f = d.fs + (long)b * (N + 1) * nx;
-        for (int i = 0; i < nx; ++i) f[i] = feas ? 0.0 : x0[(long)b * nx + i] - y[i];
-      }
-    }
   }
 }
 
@@ -314,12 +340,14 @@ __device__ __forceinline__ bool bad(double v) { return isnan(v) || isinf(v) || v
 // L: masked factor of the final free set (so that K = Quu_ff^-1 Qxu_f^T is
 // a masked solve), clamped: final clamped flags.  Returns false on LLT
 // failure ("backward_error").
-__device__ __forceinline__ bool boxqp_reg(const DevConsts& C, const double (&H)[NU * NU], const double (&q)[NU],
+__device__ __forceinline__ bool boxqp_reg(const DevConsts& C, const double* __restrict__ H, const double (&q)[NU],
                                           const double (&lb)[NU], const double (&ub)[NU], double (&x)[NU],
                                           double (&L)[28], bool (&clamped)[NU]) {
 #pragma unroll
   for (int i = 0; i < NU; ++i) x[i] = fmax(fmin(x[i], ub[i]), lb[i]);
   bool have = false;
+  double xs_f[NU];  // free-set Newton target for the current free set (cached)
+#pragma unroll 1
   for (int it = 0; it < C.qp_maxiter; ++it) {
     double g[NU];
 #pragma unroll
@@ -337,6 +365,9 @@ __device__ __forceinline__ bool boxqp_reg(const DevConsts& C, const double (&H)[
       clamped[j] = c;
     }
     if (changed) {
+      // new free set: refactor and re-solve.  While the free set is unchanged
+      // the clamped x stay at their bounds, so the right-hand side
+      // -q_f - H_fc x_c and hence the Newton target are unchanged.
 #pragma unroll
       for (int i = 0; i < NU; ++i)
 #pragma unroll
@@ -345,17 +376,19 @@ __device__ __forceinline__ bool boxqp_reg(const DevConsts& C, const double (&H)[
                                                       : (i == j ? 1.0 : 0.0);
       if (!chol_packed<NU>(L)) return false;
       have = true;
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        double acc = -q[i];
+#pragma unroll
+        for (int j = 0; j < NU; ++j)
+          if (clamped[j]) acc -= H[i * NU + j] * x[j];
+        xs_f[i] = clamped[i] ? 0.0 : acc;
+      }
+      chol_solve<NU>(L, xs_f);
     }
     double dx[NU];
 #pragma unroll
-    for (int i = 0; i < NU; ++i) {
-      double acc = -q[i];
-#pragma unroll
-      for (int j = 0; j < NU; ++j)
-        if (clamped[j]) acc -= H[i * NU + j] * x[j];
-      dx[i] = clamped[i] ? 0.0 : acc;
-    }
-    chol_solve<NU>(L, dx);
+    for (int i = 0; i < NU; ++i) dx[i] = xs_f[i];
     double dmax = 0.0;
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
@@ -376,6 +409,7 @@ __device__ __forceinline__ bool boxqp_reg(const DevConsts& C, const double (&H)[
       }
       fold = 0.5 * a1 + a2;
     }
+#pragma unroll 1
     for (int ia = 0; ia < NTRIALS; ++ia) {
       const double al = C.alphas[ia];
       double xn[NU];
@@ -429,7 +463,8 @@ template <bool FF> struct BwGroup {
   double Quu[49];
   double L[28];
   double K[7 * NX];  // K[c][j]
-  double Qu[7], kk[7], fs[NX], Vx[NX];
+  double Vxx[NX * NX];  // V_xx' (column j written/read by lane j only)
+  double Qu[7], kk[7], fs[NX], Vx[NX], Qx[NX];
   int flag;
   int clamped[7];
 };
@@ -453,7 +488,11 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
   }
   const bool active = !finished;
   const bool feas = active ? st->is_feasible != 0 : true;
+#ifdef FFDDP_EXP_NOQP
+  const bool use_qp = false;  // ablation build only (timing experiment)
+#else
   const bool use_qp = C.use_box && feas;
+#endif
   const double dt = C.dt, dt2 = C.dt * C.dt;
   const double* recb = d.rec_buf + (long)(active ? b : 0) * (N + 1) * d.rec;
   const int rec = d.rec;
@@ -472,7 +511,6 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
     bool failed = false;
     const bool work0 = !finished;
     dg = dq = stop = 0.0;
-    double Vcol[NX];
     double vx_j = 0.0;
     // ---- terminal node: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N) ----
     if (work0 && j < NX) {
@@ -481,8 +519,9 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
       double vfs = 0.0;
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
-        Vcol[i] = rT[rec_off_Lxx(NX) + i * NX + j] + (i == j ? preg : 0.0);
-        vfs += Vcol[i] * fsN[i];
+        const double v = rT[rec_off_Lxx(NX) + i * NX + j] + (i == j ? preg : 0.0);
+        S.Vxx[i * NX + j] = v;
+        vfs += v * fsN[i];
       }
       const double fj = fsN[j];
       vx_j = rT[rec_off_Lx(NX) + j] + (feas ? 0.0 : vfs);
@@ -502,9 +541,11 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
         if (j < NX) S.fs[j] = d.fs[((long)b * (N + 1) + t) * NX + j];
       }
       __syncthreads();
-      double Arow[7];
       if (work && j < NX) {
         // ---- T1 = Fx^T Vxx' (column j), T2 = Fu^T Vxx' (column j), Qx ----
+        double Vcol[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) Vcol[i] = S.Vxx[i * NX + j];
         double W[7];
 #pragma unroll
         for (int m = 0; m < 7; ++m) W[m] = dt2 * Vcol[m] + dt * Vcol[m + 7];
@@ -528,19 +569,20 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
           }
           S.T2[c * NX + j] = acc;
         }
-#pragma unroll
-        for (int m = 0; m < 7; ++m) Arow[m] = S.A[j * 7 + m];
       }
       __syncthreads();
-      double qx_j = 0.0;
       if (work && j < NX) {
+        double Arow[7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) Arow[m] = S.A[j * 7 + m];
         double wv[7];
 #pragma unroll
         for (int m = 0; m < 7; ++m) wv[m] = dt2 * S.Vx[m] + dt * S.Vx[m + 7];
-        qx_j = r[rec_off_Lx(NX) + j] + ((j < 14) ? S.Vx[j] : C.alpha * S.Vx[j]);
+        double qx_j = r[rec_off_Lx(NX) + j] + ((j < 14) ? S.Vx[j] : C.alpha * S.Vx[j]);
         if (j >= 7 && j < 14) qx_j += dt * S.Vx[j - 7];
 #pragma unroll
         for (int m = 0; m < 7; ++m) qx_j += Arow[m] * wv[m];
+        S.Qx[j] = qx_j;
         if (j < 7) {
           double qu = r[rec_off_Lu(NX) + j];
           if (FF) {
@@ -558,6 +600,9 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
       __syncthreads();
       if (work && j < NX) {
         // ---- Qxx column j = Lxx + T1 Fx ; Qxu row j = Lxu + T1 Fu ; Quu column j ----
+        double Arow[7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) Arow[m] = S.A[j * 7 + m];
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
           double acc = r[rec_off_Lxx(NX) + i * NX + j];
@@ -597,9 +642,7 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
       __syncthreads();
       // ---- gains: Eigen::LLT (infeasible) or BoxQP (feasible, bounded) ----
       if (work && j == 0) {
-        double H[NU * NU];
-#pragma unroll
-        for (int e = 0; e < NU * NU; ++e) H[e] = S.Quu[e];
+        const double* H = S.Quu;  // stays in LDS (register pressure)
         bool ok;
         if (!use_qp) {
           double L[28];
@@ -675,11 +718,11 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
             a2 -= qxu_j[c] * S.K[c * NX + i];
           }
           const double v = 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
-          Vcol[i] = v;
+          S.Vxx[i * NX + j] = v;
           vfs += v * S.fs[i];
           badv |= bad(fabs(v)) ? 1 : 0;
         }
-        double vx = qx_j;
+        double vx = S.Qx[j];
 #pragma unroll
         for (int c = 0; c < 7; ++c) vx -= Kcol[c] * S.Qu[c];
         if (!feas) vx += vfs;
@@ -1126,7 +1169,7 @@ template <class T> int dalloc(ffddp_handle* h, T** p, size_t n) {
 }
 
 void free_all(ffddp_handle* h) {
-  void* ps[] = {h->dc, h->drb, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
+  void* ps[] = {h->dc, h->drb, h->d.prim, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
                 h->d.us_try, h->d.trial, h->d.trial_fail, h->d.st, h->in_x0, h->in_nref, h->in_iref, h->in_xs,
                 h->in_us, h->in_surf, h->out_xs, h->out_us, h->out_K, h->out_cost, h->out_fn, h->out_iters,
                 h->out_stats, h->out_ok};
@@ -1177,6 +1220,8 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
   for (int it = 0; it < maxiter; ++it) {
     {
       ProfScope p(h, s, KC_NODE);
+      hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, s, h->dc, d, x0, nref, iref,
+                         surf, 0);
       hipLaunchKernelGGL((k_node<NC, FF>), dim3(node_blocks), dim3(NODE_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf, 0);
     }
     {
@@ -1227,6 +1272,8 @@ int launch_solve(ffddp_handle* h, int B, const double* x0, const double* nref, c
 template <int NC, bool FF>
 void launch_node(ffddp_handle* h, Dev d, int B, hipStream_t s, int force_all) {
   const long nodes = (long)B * (h->hc.N + 1);
+  hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
+                     h->in_nref, h->in_iref, h->in_surf, force_all);
   hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, s, h->dc,
                      d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all);
 }
@@ -1274,6 +1321,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   rc |= dalloc(h, &d.trial, (size_t)B * NTRIALS * 2);
   rc |= dalloc(h, &d.trial_fail, (size_t)B * NTRIALS);
   rc |= dalloc(h, &d.st, (size_t)B);
+  rc |= dalloc(h, &d.prim, (size_t)B * (N + 1));
   rc |= dalloc(h, &h->in_x0, (size_t)B * nx);
   rc |= dalloc(h, &h->in_nref, (size_t)B * (N + 1) * 6);
   rc |= dalloc(h, &h->in_iref, (size_t)B * 21);

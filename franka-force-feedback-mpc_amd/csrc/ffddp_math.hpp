@@ -108,20 +108,27 @@ template <class T> FFD_HD V3<T> cmul(const double* I, V3<T> x) {
 }
 
 // ---------------------------------------------------------------------------
-// packed lower-triangular Cholesky (Eigen::LLT semantics: fail if pivot <= 0)
+// packed lower-triangular Cholesky (Eigen::LLT semantics: fail if pivot <= 0).
+// Storage: off-diagonal L_ij (i > j) as usual, the DIAGONAL HOLDS 1 / L_ii so
+// that the triangular solves multiply instead of divide (fp64 division is a
+// ~10-instruction dependent sequence on CDNA; the solves sit on the critical
+// path of every kernel).
 // ---------------------------------------------------------------------------
 FFD_HD int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
 template <int N> FFD_HD bool chol_packed(double* A /* packed lower, in-place */) {
+#pragma unroll
   for (int j = 0; j < N; ++j) {
     double d = A[tri(j, j)];
+#pragma unroll
     for (int k = 0; k < j; ++k) d -= A[tri(j, k)] * A[tri(j, k)];
     if (!(d > 0.0)) return false;
-    const double l = sqrt(d);
-    A[tri(j, j)] = l;
-    const double il = 1.0 / l;
+    const double il = 1.0 / sqrt(d);
+    A[tri(j, j)] = il;
+#pragma unroll
     for (int i = j + 1; i < N; ++i) {
       double s = A[tri(i, j)];
+#pragma unroll
       for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
       A[tri(i, j)] = s * il;
     }
@@ -130,18 +137,22 @@ template <int N> FFD_HD bool chol_packed(double* A /* packed lower, in-place */)
 }
 // solve L y = b in place
 template <int N> FFD_HD void fwd_sub(const double* L, double* b) {
+#pragma unroll
   for (int i = 0; i < N; ++i) {
     double s = b[i];
+#pragma unroll
     for (int k = 0; k < i; ++k) s -= L[tri(i, k)] * b[k];
-    b[i] = s / L[tri(i, i)];
+    b[i] = s * L[tri(i, i)];
   }
 }
 // solve L^T x = y in place
 template <int N> FFD_HD void bwd_sub(const double* L, double* b) {
+#pragma unroll
   for (int i = N - 1; i >= 0; --i) {
     double s = b[i];
+#pragma unroll
     for (int k = i + 1; k < N; ++k) s -= L[tri(k, i)] * b[k];
-    b[i] = s / L[tri(i, i)];
+    b[i] = s * L[tri(i, i)];
   }
 }
 template <int N> FFD_HD void chol_solve(const double* L, double* b) {

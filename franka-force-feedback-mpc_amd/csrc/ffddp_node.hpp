@@ -133,6 +133,58 @@ struct Primal {
   double xnext[14];
 };
 
+// field-wise copy (static indices only, so a register-resident Primal is not
+// forced into scratch memory by a whole-struct memcpy)
+FFD_HD void copy_primal(const Primal& s, Primal& d) {
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) d.a[i] = s.a[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d.lam[i] = s.lam[i];
+#pragma unroll
+  for (int i = 0; i < 28; ++i) d.L[i] = s.L[i];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      d.Jc[r][i] = s.Jc[r][i];
+      d.Y[r][i] = s.Y[r][i];
+    }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) d.Ls[i] = s.Ls[i];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      d.z[i][k] = s.z[i][k];
+      d.o[i][k] = s.o[i][k];
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    d.pee[i] = s.pee[i];
+    d.r_rot[i] = s.r_rot[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) d.Ree[i] = s.Ree[i];
+  d.th_rot = s.th_rot;
+#pragma unroll
+  for (int i = 0; i < NDENSE_MAX; ++i) {
+    d.D[i] = s.D[i];
+    d.g[i] = s.g[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    d.Dx[i] = s.Dx[i];
+    d.gx[i] = s.gx[i];
+    d.xnext[i] = s.xnext[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    d.Du[i] = s.Du[i];
+    d.gu[i] = s.gu[i];
+  }
+  d.cost = s.cost;
+}
+
 // n-dim force vector in world coordinates from lambda
 template <int NC> FFD_HD void force_world(const double* lam, double* fw) {
   if (NC == 1) {
@@ -164,6 +216,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   } else {
     rb_pass<double, false, false>(C.rb, q, v, zero, nullptr, K, nullptr);
   }
+  #pragma unroll
   for (int i = 0; i < NQ; ++i) {
     P.z[i][0] = K.z[i].x;
     P.z[i][1] = K.z[i].y;
@@ -175,13 +228,16 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   P.pee[0] = K.pee.x;
   P.pee[1] = K.pee.y;
   P.pee[2] = K.pee.z;
+  #pragma unroll
   for (int k = 0; k < 9; ++k) P.Ree[k] = K.Ree.m[k];
   const double pstar[3] = {ref[0], ref[1], ref[2] - C.z_press};
   P.lam[0] = P.lam[1] = P.lam[2] = 0.0;
   if (with_dyn) {
+    #pragma unroll
     for (int k = 0; k < 28; ++k) P.L[k] = M[k];
     chol_packed<NQ>(P.L);  // M is SPD for the arm
     double af[NQ];
+    #pragma unroll
     for (int i = 0; i < NQ; ++i) af[i] = u[i] - K.tau[i];
     chol_solve<NQ>(P.L, af);
     if (surface) {
@@ -190,9 +246,11 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
       double gam[3];
       const double ap[3] = {K.ap.x, K.ap.y, K.ap.z};
       const double vp[3] = {K.vp.x, K.vp.y, K.vp.z};
+      #pragma unroll
       for (int r = 0; r < nc; ++r) {
         const int cmp = c0 + r;
         gam[r] = ap[cmp] + C.Kp * (P.pee[cmp] - pstar[cmp]) + C.Kd * vp[cmp];
+        #pragma unroll
         for (int i = 0; i < NQ; ++i) {
           const double dx = P.pee[0] - P.o[i][0], dy = P.pee[1] - P.o[i][1], dz = P.pee[2] - P.o[i][2];
           const double cr[3] = {P.z[i][1] * dz - P.z[i][2] * dy, P.z[i][2] * dx - P.z[i][0] * dz,
@@ -201,21 +259,29 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
         }
       }
       // Y = L^-1 Jc^T, S = Y^T Y + eps I
+      #pragma unroll
       for (int r = 0; r < nc; ++r) {
+        #pragma unroll
         for (int i = 0; i < NQ; ++i) P.Y[r][i] = P.Jc[r][i];
         fwd_sub<NQ>(P.L, P.Y[r]);
       }
       double S[6];
+      #pragma unroll
       for (int r = 0; r < nc; ++r)
+        #pragma unroll
         for (int s = 0; s <= r; ++s) {
           double acc = 0.0;
+          #pragma unroll
           for (int i = 0; i < NQ; ++i) acc += P.Y[r][i] * P.Y[s][i];
           S[tri(r, s)] = acc + (r == s ? C.eps : 0.0);
         }
+      #pragma unroll
       for (int k = 0; k < 6; ++k) P.Ls[k] = S[k];
       double yl[3];
+      #pragma unroll
       for (int r = 0; r < nc; ++r) {
         double acc = gam[r];
+        #pragma unroll
         for (int i = 0; i < NQ; ++i) acc += P.Jc[r][i] * af[i];
         yl[r] = acc;
       }
@@ -223,27 +289,36 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
       chol_solve<NC>(P.Ls, yl);
       // lambda = -y_l ;  a = af + M^-1 Jc^T lambda
       double t7[NQ];
+      #pragma unroll
       for (int i = 0; i < NQ; ++i) {
         double acc = 0.0;
+        #pragma unroll
         for (int r = 0; r < nc; ++r) acc += P.Jc[r][i] * (-yl[r]);
         t7[i] = acc;
       }
       chol_solve<NQ>(P.L, t7);
+      #pragma unroll
       for (int i = 0; i < NQ; ++i) P.a[i] = af[i] + t7[i];
+      #pragma unroll
       for (int r = 0; r < nc; ++r) P.lam[r] = -yl[r];
     } else {
+      #pragma unroll
       for (int i = 0; i < NQ; ++i) P.a[i] = af[i];
     }
   }
 
   // ---------------- costs (CostModelSum, in _make_dam order) ----------------
   double cost = 0.0;
+  #pragma unroll
   for (int k = 0; k < NDENSE_MAX; ++k) P.D[k] = P.g[k] = 0.0;
+  #pragma unroll
   for (int k = 0; k < 14; ++k) P.Dx[k] = P.gx[k] = 0.0;
+  #pragma unroll
   for (int k = 0; k < 7; ++k) P.Du[k] = P.gu[k] = 0.0;
   if (C.variant == FFDDP_CLASSICAL || C.inner_state_reg) {
     // posture: Quad on x - x_reg_ref
     double a = 0.0;
+    #pragma unroll
     for (int i = 0; i < 14; ++i) {
       const double r = x[i] - xreg[i];
       a += r * r;
@@ -253,6 +328,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
     cost += C.w_post * (0.5 * a);
     // v_damp: WeightedQuad [0*7, vdw] on x - 0
     a = 0.0;
+    #pragma unroll
     for (int i = 0; i < 14; ++i) {
       const double wi = i < 7 ? 0.0 : C.vdw[i - 7];
       a += wi * x[i] * x[i];
@@ -263,6 +339,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   }
   if (C.has_qsoft) {
     double a = 0.0;
+    #pragma unroll
     for (int i = 0; i < 14; ++i) {
       double ai, Ar, Arr;
       barrier(x[i] - C.qs_xref[i], C.qs_lb[i], C.qs_ub[i], ai, Ar, Arr);
@@ -274,12 +351,15 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   }
   {  // ee_ori: FrameRotation(R_des), WeightedQuad(ori_weights)
     double Rrel[9];
+    #pragma unroll
     for (int i = 0; i < 3; ++i)
+      #pragma unroll
       for (int j = 0; j < 3; ++j)
         Rrel[3 * i + j] = C.Rdes[0 * 3 + i] * P.Ree[0 * 3 + j] + C.Rdes[1 * 3 + i] * P.Ree[1 * 3 + j] +
                           C.Rdes[2 * 3 + i] * P.Ree[2 * 3 + j];
     log3(Rrel, P.r_rot, P.th_rot);
     double a = 0.0;
+    #pragma unroll
     for (int i = 0; i < 3; ++i) {
       a += C.ori_w[i] * P.r_rot[i] * P.r_rot[i];
       P.D[3 + i] += C.w_ori * C.ori_w[i];
@@ -290,6 +370,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   const double vel[6] = {K.vp.x, K.vp.y, K.vp.z, K.w.x, K.w.y, K.w.z};
   {  // w_damp: FrameVelocity(0, LWA), WeightedQuad [0,0,0, ww]
     double a = 0.0;
+    #pragma unroll
     for (int i = 0; i < 3; ++i) {
       a += C.wd_w[i] * vel[3 + i] * vel[3 + i];
       P.D[9 + i] += C.w_wd * C.wd_w[i];
@@ -299,6 +380,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   }
   if (!terminal && (C.variant == FFDDP_CLASSICAL || C.inner_tau_reg)) {
     double a = 0.0;
+    #pragma unroll
     for (int i = 0; i < 7; ++i) {
       const double r = u[i] - tauref[i];
       a += r * r;
@@ -308,6 +390,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
     cost += C.w_tau * (0.5 * a);
     if (C.has_tsoft) {
       a = 0.0;
+      #pragma unroll
       for (int i = 0; i < 7; ++i) {
         double ai, Ar, Arr;
         barrier(u[i], C.ts_lb[i], C.ts_ub[i], ai, Ar, Arr);
@@ -321,6 +404,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   if (!surface) {
     // ee_pos: FrameTranslation(p_ref), WeightedQuad [1,1,2.5]
     double a = 0.0;
+    #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const double r = P.pee[i] - ref[i];
       a += C.ee_pos_w[i] * r * r;
@@ -361,9 +445,11 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
     // contact force: lambda (classical terminal calc(x): zero-initialised data, R2)
     double lam[3] = {0, 0, 0};
     if (mode != MODE_TERMINAL_X)
+      #pragma unroll
       for (int r = 0; r < nc; ++r) lam[r] = P.lam[r];
     if (C.has_uni) {
       double a = 0.0;
+      #pragma unroll
       for (int r = 0; r < nc; ++r) {
         double ai, Ar, Arr;
         barrier(lam[r], C.uni_lb[r], C.uni_ub[r], ai, Ar, Arr);
@@ -375,6 +461,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
     }
     if (C.has_fn) {
       double a = 0.0;
+      #pragma unroll
       for (int r = 0; r < nc; ++r) {
         const double rr = lam[r] - C.fn_ref[r];
         a += C.fn_w[r] * rr * rr;
@@ -387,12 +474,14 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   P.cost = cost;
   if (with_dyn) {
     const double dt = C.dt;
+    #pragma unroll
     for (int i = 0; i < NQ; ++i) {
       const double vn = v[i] + P.a[i] * dt;
       P.xnext[i] = q[i] + (v[i] * dt + P.a[i] * dt * dt);
       P.xnext[NQ + i] = vn;
     }
   } else {
+    #pragma unroll
     for (int i = 0; i < 14; ++i) P.xnext[i] = x[i];
   }
 }
