@@ -208,8 +208,8 @@ def main():
         if tf.exists():
             try:
                 tj = json.loads(tf.read_text())
-                if tj.get("kernel") == dom and tj.get("config") == f"{args.variant}/{args.contact}/B{B}/N{N}":
-                    traffic = tj.get("hbm_bytes_per_launch")
+                if tj.get("config") == f"{args.variant}/{args.contact}/B{B}/N{N}":
+                    traffic = tj.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         roofline = {

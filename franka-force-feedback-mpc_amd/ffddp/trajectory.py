@@ -4,7 +4,7 @@ Restates src/tasks/trajectories.py:8-93 (make_approach_then_circle) and the
 benchmark-mode wrapper of src/run/run_classical.py:221-264 (contact height,
 pre/approach timing and the 0.2 s hold at contact onset).  Pinned by golden
 vectors generated from the reference module itself (tests/golden/
-make_golden.py -> trajectory.npz).
+make_golden.py -> reference_vectors.npz).
 """
 from __future__ import annotations
 
