@@ -112,21 +112,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP-event timing")
+    ap.add_argument("--no-host-io", action="store_true", help="skip the PCIe-inclusive host-array rate")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
-    from ffddp import BatchedBoxFDDP, _abi, robot as R, workload
+    from ffddp import BatchedBoxFDDP, _abi, robot as R, shard, workload
     from ffddp.config import classical_preset, ff_preset
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    rank, world, local_rank = shard.env_ranks()
+    shard.init("nccl", local_rank, world)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
@@ -135,7 +131,8 @@ def main():
     nx, nu = cfg.nx, 7
     ee = R.R_MJ_FROM_PIN @ _abi.frame_placement(R.Q_NEUTRAL)[1]
     batch = workload.make_batch(
-        B, N, args.variant, _abi.gravity_torque, ee, seed=1234 + rank, regime=args.regime, fk=_abi.frame_placement
+        B, N, args.variant, _abi.gravity_torque, ee, seed=shard.shard_seed(1234, rank), regime=args.regime,
+        fk=_abi.frame_placement,
     )
     f64 = dict(dtype=torch.float64, device=dev)
     T = dict(
@@ -161,8 +158,7 @@ def main():
     def step():
         solver.solve_dev(T, maxiter=args.maxiter, is_feasible=False, stream=stream)
         if world > 1:  # final exchange: per-instance cost + first control to every rank
-            local = torch.cat([T["cost"][:, None], T["us"][:, 0, :]], 1)
-            dist.all_gather_into_tensor(gathered, local)
+            shard.gather_results(T["cost"], T["us"][:, 0, :], gathered)
 
     for _ in range(args.warmup):
         step()
@@ -170,20 +166,7 @@ def main():
     if not args.no_profile:
         solver.profile(True)
         solver.profile_read(reset=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.timed_steps(step, args.steps, lambda: torch.cuda.synchronize(dev))
     prof = solver.profile_read(reset=True) if not args.no_profile else None
 
     stats = T["stats"].cpu().numpy()
@@ -225,6 +208,20 @@ def main():
             "frac_of_measured_copy": achieved / HBM_MEASURED_GBS,
         }
 
+    host_io = None
+    if not args.no_host_io:
+        # PCIe-inclusive rate of the host-array entry point (ffddp_solve_batch):
+        # H2D of the inputs + solve + D2H of xs/us/K/cost/...; reported beside
+        # `value`, never as `value`.
+        solver.profile(False)
+        solver.solve(batch, maxiter=args.maxiter)
+        th0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            solver.solve(batch, maxiter=args.maxiter)
+        th = (time.perf_counter() - th0) / reps
+        host_io = {"value": B / th, "unit": "solves/s", "ms_per_step": th * 1e3, "per_gpu": True}
+
     if rank == 0:
         base = None
         if not args.no_cpu_baseline and world == 1:
@@ -264,6 +261,7 @@ def main():
                 "cost_finite_frac": float(np.mean(np.isfinite(cost))),
             },
             "kernels": kernels,
+            "host_io": host_io,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

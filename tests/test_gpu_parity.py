@@ -95,3 +95,23 @@ def test_gravity_torque_dev_matches_oracle():
     assert rc == 0
     torch.cuda.synchronize()
     assert rel_err(td.cpu().numpy(), P.gravity_torque(q)) < 1e-12
+
+
+@pytest.mark.parametrize("box,regime", [(False, "tracking"), (True, "random")])
+def test_solve_variants_match_oracle(box, regime):
+    """Plain FDDP (use_box_fddp=False: Cholesky gains, no clamping, th_stop 1e-9)
+    and the SURVEY-literal random x0 regime."""
+    N, B = 20, 4
+    cfg = product_cfg("classical", N)
+    cfg.use_box_fddp = box
+    b = make_batch("classical", B, N, seed=33, surface=1, regime=regime)
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    ok = solver.solve(b, maxiter=10, is_feasible=False)
+    for i in range(B):
+        ok_o, s = oracle_solve(cfg, b, i, box=box)
+        assert bool(ok[i]) == bool(ok_o)
+        assert int(solver.iter[i]) == int(s.iter), (i, solver.iter[i], s.iter)
+        assert rel_err(solver.cost[i], s.cost) < TOL_SOLVE
+        assert rel_err(solver.xs[i], s.xs) < TOL_SOLVE
+        assert rel_err(solver.us[i], s.us) < TOL_SOLVE
+        assert rel_err(solver.K[i], s.K) < TOL_SOLVE * 10
