@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -36,6 +37,9 @@ constexpr int NODE_BLOCK = 256;
 constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 constexpr int BW_BLOCK = 64;
 constexpr int FW_BLOCK = 64;
+#ifndef BW_WAVES
+#define BW_WAVES 1
+#endif
 
 struct InstState {
   double preg, cost, dg, dq, stop;
@@ -799,6 +803,546 @@ __global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restri
 }
 
 // ---------------------------------------------------------------------------
+// backward pass, one wavefront per instance (k_backward_w)
+//
+// The Riccati recursion of one instance is a chain of 30 small dense steps;
+// what bounds it is latency, not flops.  One wave (64 lanes) owns one
+// instance and spreads each step's algebra over all lanes:
+//   [Fx Fu] = I~ + D A^        (Euler structure: I~ sparse, D = [dt^2 I; dt I],
+//                               A^ = node acceleration Jacobian, 7 x (nx+nu))
+//   Q = L + I~'V I~ + M A^ + (M A^)',   M = I~'(V D) + 1/2 A^'(D'V D)
+// so the full Q (x and u blocks) is one symmetric rank-7 update plus sparse
+// terms; every lane computes a few lower-triangle entries.  The node record
+// for t-1 is prefetched into registers while node t is processed (LDS-only
+// fences between phases, so the prefetch stays in flight), and with no
+// per-lane arrays beyond that the kernel fits several waves per SIMD, so
+// instances hide each other's latency.  Gains (LLT / BoxQP on 7x7) stay on
+// lane 0.
+// ---------------------------------------------------------------------------
+constexpr int rec_words(int nx) { return ((147 + nx * nx + nx * 7 + 49 + nx + 7 + 1) + 3 + 7) & ~7; }
+
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <bool FF> struct BwW {
+  static constexpr int NX = FF ? 21 : 14;
+  static constexpr int ND = NX + NU;
+  static constexpr int REC = rec_words(NX);
+  double R[REC];      // staged node record (A | Lxx | Lxu | Luu | Lx | Lu | cost | lam)
+  double V[NX * NX];  // V_xx' on entry to a node, V_xx on exit
+  double Q[ND * ND];  // [[Qxx, Qxu], [Qux, Quu + preg I]]
+  double W[NX * NU];  // V D
+  double Y[NU * NU];  // D' V D
+  double M[ND * NU];
+  double K[NU * NX];
+  double H[NU * NU];  // Quu + preg I (contiguous copy for the gains lane)
+  double L[28];       // packed (masked) Cholesky factor, reciprocal diagonal
+  double Vx[NX], Qv[ND], fs[NX], kk[NU], z[NU], kp[NU], uu[NU];
+  int flag;
+  int clamped[NU];
+};
+
+// nonzeros of column c of I~ (the Euler identity part of [Fx Fu]):
+// returns the count and fills (row, coef) pairs.
+template <bool FF> __device__ __forceinline__ int itilde(int c, double dt, double alpha, double beta, int (&row)[2],
+                                                         double (&cf)[2]) {
+  if (c < 7) {
+    row[0] = c;
+    cf[0] = 1.0;
+    return 1;
+  }
+  if (c < 14) {
+    row[0] = c;
+    cf[0] = 1.0;
+    row[1] = c - 7;
+    cf[1] = dt;
+    return 2;
+  }
+  if (!FF) return 0;  // classical u columns: Fu = D A_u only
+  if (c < 21) {
+    row[0] = c;
+    cf[0] = alpha;
+    return 1;
+  }
+  row[0] = c - 7;
+  cf[0] = beta;
+  return 1;
+}
+
+// A^[m][c] = d a_m / d dir_c (record rows 0..20; FF w-columns 21..27 are zero)
+template <bool FF> __device__ __forceinline__ double ahat(const double* Ar, int m, int c) {
+  return (FF && c >= 21) ? 0.0 : Ar[c * 7 + m];
+}
+
+// lower-triangle index e -> (r, c), r >= c
+__device__ __forceinline__ void tri_rc(int e, int& r, int& c) {
+  int rr = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+  while ((rr + 1) * (rr + 2) / 2 <= e) ++rr;
+  while (rr * (rr + 1) / 2 > e) --rr;
+  r = rr;
+  c = e - rr * (rr + 1) / 2;
+}
+
+// ---- 7x7 algebra with one row / variable per lane (lanes 0..6), uniform control flow ----
+__device__ __forceinline__ double bcast(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// In-place LLT of the SPD matrix whose row i is held by lane i: on exit
+// a[j] (j < i) = L_ij and a[i] = 1 / L_ii (same operation order as
+// chol_packed).  Returns false (uniformly) at the first non-positive pivot.
+__device__ __forceinline__ bool chol_rows(double (&a)[NU], int lane) {
+#pragma unroll
+  for (int k = 0; k < NU; ++k) {
+    double d = a[k];
+#pragma unroll
+    for (int m = 0; m < k; ++m) d -= a[m] * a[m];
+    const double dk = bcast(d, k);
+    if (!(dk > 0.0)) return false;
+    const double il = 1.0 / sqrt(dk);
+    double s = a[k];
+#pragma unroll
+    for (int m = 0; m < k; ++m) s -= a[m] * bcast(a[m], k);
+    a[k] = (lane == k) ? il : ((lane > k) ? s * il : a[k]);
+  }
+  return true;
+}
+
+// solve L L^T x = r with L held as rows (chol_rows layout); r / result per lane
+__device__ __forceinline__ double chol_solve_rows(const double (&Lr)[NU], double r, int lane) {
+  double y[NU];
+#pragma unroll
+  for (int k = 0; k < NU; ++k) {
+    double s = r;
+#pragma unroll
+    for (int m = 0; m < k; ++m) s -= Lr[m] * y[m];
+    y[k] = bcast(s * Lr[k], k);
+  }
+  double x[NU];
+#pragma unroll
+  for (int k = NU - 1; k >= 0; --k) {
+    double s = y[k];
+#pragma unroll
+    for (int m = k + 1; m < NU; ++m) s -= bcast(Lr[k], m) * x[m];
+    x[k] = s * bcast(Lr[k], k);
+  }
+  double out = 0.0;
+#pragma unroll
+  for (int k = 0; k < NU; ++k) out = (lane == k) ? x[k] : out;
+  return out;
+}
+
+// crocoddyl::BoxQP::solve with variable i on lane i (see boxqp_reg for the
+// algorithm).  hrow = row i of H; x in = warm start, out = solution; Lr = rows
+// of the masked factor of the final free set; clmask = final clamped set.
+__device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&hrow)[NU], double q, double lb,
+                                            double ub, double& x, double (&Lr)[NU], int& clmask, int lane) {
+  x = fmax(fmin(x, ub), lb);
+  bool have = false, cl = false;
+  double xsf = 0.0;
+  double qb[NU];
+#pragma unroll
+  for (int j = 0; j < NU; ++j) qb[j] = bcast(q, j);
+#pragma unroll 1
+  for (int it = 0; it < C.qp_maxiter; ++it) {
+    double xb[NU];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) xb[j] = bcast(x, j);
+    double g = q;
+#pragma unroll
+    for (int j = 0; j < NU; ++j) g += hrow[j] * xb[j];
+    const bool c = (x == lb && g > 0.0) || (x == ub && g < 0.0);
+    const bool changed = !have || ((__ballot(c != cl) & 0x7Full) != 0);
+    cl = c;
+    if (changed) {
+      const int m = (int)(__ballot(cl) & 0x7Full);
+#pragma unroll
+      for (int j = 0; j < NU; ++j) {
+        const bool cj = (m >> j) & 1;
+        Lr[j] = (!cl && !cj) ? hrow[j] + (lane == j ? C.qp_reg : 0.0) : (lane == j ? 1.0 : 0.0);
+      }
+      if (!chol_rows(Lr, lane)) return false;
+      have = true;
+      double r = -q;
+#pragma unroll
+      for (int j = 0; j < NU; ++j)
+        if ((m >> j) & 1) r -= hrow[j] * xb[j];
+      xsf = chol_solve_rows(Lr, cl ? 0.0 : r, lane);
+      clmask = m;
+    }
+    const double dx = cl ? 0.0 : xsf - x;
+    double dmax = 0.0;
+    double dxb[NU], gb[NU];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+      dxb[j] = bcast(dx, j);
+      gb[j] = bcast(g, j);
+      dmax = fmax(dmax, fabs(dxb[j]));
+    }
+    if (dmax < C.qp_th_grad) break;
+    double fold;
+    {
+      double hx = 0.0;
+#pragma unroll
+      for (int j = 0; j < NU; ++j) hx += hrow[j] * xb[j];
+      double a1 = 0.0, a2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        a1 += xb[i] * bcast(hx, i);
+        a2 += qb[i] * xb[i];
+      }
+      fold = 0.5 * a1 + a2;
+    }
+#pragma unroll 1
+    for (int ia = 0; ia < NTRIALS; ++ia) {
+      const double al = C.alphas[ia];
+      const double xn = fmax(fmin(x + al * dx, ub), lb);
+      double xnb[NU];
+#pragma unroll
+      for (int j = 0; j < NU; ++j) xnb[j] = bcast(xn, j);
+      double hxn = 0.0;
+#pragma unroll
+      for (int j = 0; j < NU; ++j) hxn += hrow[j] * xnb[j];
+      double a1 = 0.0, a2 = 0.0, gd = 0.0;
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        a1 += xnb[i] * bcast(hxn, i);
+        a2 += qb[i] * xnb[i];
+        gd += gb[i] * (xb[i] - xnb[i]);
+      }
+      if (fold - (0.5 * a1 + a2) > C.qp_th_acceptstep * gd) {
+        x = xn;
+        break;
+      }
+    }
+  }
+  return true;
+}
+
+template <bool FF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_WAVES))) void k_backward_w(const DevConsts* __restrict__ Cg, Dev d, int iter) {
+  using S_t = BwW<FF>;
+  constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
+  constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  const int b = blockIdx.x, l = threadIdx.x;
+  if (b >= d.B) return;
+  InstState* st = d.st + b;
+  if (st->done) return;
+  __shared__ S_t S;
+  const bool feas = st->is_feasible != 0;
+#ifdef FFDDP_EXP_NOQP
+  const bool use_qp = false;
+#else
+  const bool use_qp = C.use_box && feas;
+#endif
+  const double dt = C.dt, dt2 = C.dt * C.dt, alpha = C.alpha, beta = C.beta;
+  const double* recb = d.rec_buf + (long)b * (N + 1) * REC;
+  if (st->recalc) {
+    double c = 0.0;
+    for (int t = l; t <= N; t += 64) c += recb[(long)t * REC + rec_off_cost(NX)];
+    c = wave_sum(c);
+    if (l == 0) {
+      st->cost = c;
+      st->n_calc += 1;
+    }
+  }
+  double preg = st->preg;
+  int retries = 0;
+  bool fail_inst = false;
+  double dg = 0.0, dq = 0.0, stop = 0.0;
+  for (;;) {
+    dg = dq = stop = 0.0;
+    bool failed = false;
+    // ---- terminal node: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N) ----
+    {
+      const double* rT = recb + (long)N * REC;
+      for (int e = l; e < NX * NX; e += 64) {
+        const int i = e / NX, j = e % NX;
+        S.V[e] = rT[rec_off_Lxx(NX) + e] + (i == j ? preg : 0.0);
+      }
+      if (l < NX) S.fs[l] = d.fs[((long)b * (N + 1) + N) * NX + l];
+    }
+    lds_sync();
+    double pf[NPF];
+    {
+      const double* r1 = recb + (long)(N - 1) * REC;
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) pf[k] = (l + 64 * k < REC) ? r1[l + 64 * k] : 0.0;
+    }
+    double pfs = (l < NX) ? d.fs[((long)b * (N + 1) + N - 1) * NX + l] : 0.0;
+    double pkp = 0.0, pus = 0.0;
+    if (l < NU) {
+      pkp = d.k[((long)b * N + N - 1) * NU + l];
+      pus = d.us[((long)b * N + N - 1) * NU + l];
+    }
+    {
+      double cdg = 0.0, cdq = 0.0;
+      if (l < NX) {
+        const double* rT = recb + (long)N * REC;
+        double vfs = 0.0;
+        for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
+        const double fj = S.fs[l];
+        const double vx = rT[rec_off_Lx(NX) + l] + (feas ? 0.0 : vfs);
+        if (!feas) {
+          d.w[((long)b * (N + 1) + N) * NX + l] = vfs;
+          cdg = -vx * fj;
+          cdq = fj * vfs;
+        }
+        S.Vx[l] = vx;
+      }
+      dg += wave_sum(cdg);
+      dq += wave_sum(cdq);
+    }
+    lds_sync();
+    for (int t = N - 1; t >= 0; --t) {
+      // ---- stage record t (prefetched) ; start loading record t-1 ----
+#pragma unroll
+      for (int k = 0; k < NPF; ++k)
+        if (l + 64 * k < REC) S.R[l + 64 * k] = pf[k];
+      if (l < NX) S.fs[l] = pfs;
+      if (l < NU) {
+        S.kp[l] = pkp;
+        S.uu[l] = pus;
+      }
+      if (t > 0) {
+        const double* r1 = recb + (long)(t - 1) * REC;
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) pf[k] = (l + 64 * k < REC) ? r1[l + 64 * k] : 0.0;
+        if (l < NX) pfs = d.fs[((long)b * (N + 1) + t - 1) * NX + l];
+        if (l < NU) {
+          pkp = d.k[((long)b * N + t - 1) * NU + l];
+          pus = d.us[((long)b * N + t - 1) * NU + l];
+        }
+      }
+      lds_sync();
+      const double* Ar = S.R + rec_off_A();
+      // ---- phase A: W = V D, Y = D' V D, z = D' Vx ----
+      for (int e = l; e < NX * NU + NU * NU + NU; e += 64) {
+        if (e < NX * NU) {
+          const int i = e / NU, m = e % NU;
+          S.W[e] = dt2 * S.V[i * NX + m] + dt * S.V[i * NX + 7 + m];
+        } else if (e < NX * NU + NU * NU) {
+          const int f = e - NX * NU, m = f / NU, n = f % NU;
+          const double wq = dt2 * S.V[m * NX + n] + dt * S.V[m * NX + 7 + n];
+          const double wv = dt2 * S.V[(7 + m) * NX + n] + dt * S.V[(7 + m) * NX + 7 + n];
+          S.Y[f] = dt2 * wq + dt * wv;
+        } else {
+          const int m = e - NX * NU - NU * NU;
+          S.z[m] = dt2 * S.Vx[m] + dt * S.Vx[7 + m];
+        }
+      }
+      lds_sync();
+      // ---- phase B: M = I~'W + 1/2 A^'Y ; Qv = [Lx; Lu] + I~'Vx + A^'z ----
+      for (int e = l; e < ND * NU + ND; e += 64) {
+        int row[2];
+        double cf[2];
+        if (e < ND * NU) {
+          const int c = e / NU, m = e % NU;
+          const int nz = itilde<FF>(c, dt, alpha, beta, row, cf);
+          double acc = 0.0;
+          for (int q = 0; q < nz; ++q) acc += cf[q] * S.W[row[q] * NU + m];
+          double h = 0.0;
+#pragma unroll
+          for (int n = 0; n < NU; ++n) h += ahat<FF>(Ar, n, c) * S.Y[n * NU + m];
+          S.M[e] = acc + 0.5 * h;
+        } else {
+          const int c = e - ND * NU;
+          const int nz = itilde<FF>(c, dt, alpha, beta, row, cf);
+          double acc = (c < NX) ? S.R[rec_off_Lx(NX) + c] : S.R[rec_off_Lu(NX) + c - NX];
+          for (int q = 0; q < nz; ++q) acc += cf[q] * S.Vx[row[q]];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) acc += ahat<FF>(Ar, m, c) * S.z[m];
+          S.Qv[c] = acc;
+        }
+      }
+      lds_sync();
+      // ---- phase C: Q lower triangle (mirrored) ----
+      for (int e = l; e < ND * (ND + 1) / 2; e += 64) {
+        int r, c;
+        tri_rc(e, r, c);
+        double lv;
+        if (r < NX)
+          lv = S.R[rec_off_Lxx(NX) + r * NX + c];
+        else if (c < NX)
+          lv = S.R[rec_off_Lxu(NX) + c * NU + (r - NX)];
+        else
+          lv = S.R[rec_off_Luu(NX) + (r - NX) * NU + (c - NX)];
+        int rr[2], rc2[2];
+        double ar[2], ac[2];
+        const int nr = itilde<FF>(r, dt, alpha, beta, rr, ar);
+        const int nc2 = itilde<FF>(c, dt, alpha, beta, rc2, ac);
+        double g = 0.0;
+        for (int p = 0; p < nr; ++p)
+          for (int q = 0; q < nc2; ++q) g += ar[p] * ac[q] * S.V[rr[p] * NX + rc2[q]];
+        double h = 0.0;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) h += S.M[r * NU + m] * ahat<FF>(Ar, m, c) + S.M[c * NU + m] * ahat<FF>(Ar, m, r);
+        double v = lv + g + h;
+        if (r == c && r >= NX) v += preg;
+        S.Q[r * ND + c] = v;
+        S.Q[c * ND + r] = v;
+        if (c >= NX) {
+          S.H[(r - NX) * NU + (c - NX)] = v;
+          S.H[(c - NX) * NU + (r - NX)] = v;
+        }
+      }
+      lds_sync();
+      // ---- phase D: gains (Eigen::LLT or BoxQP), row / variable i on lane i ----
+      {
+        double hrow[NU], Lr[NU];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.H[l * NU + j] : (l == j ? 1.0 : 0.0);
+        bool ok;
+        if (!use_qp) {
+#pragma unroll
+          for (int j = 0; j < NU; ++j) Lr[j] = hrow[j];
+          ok = chol_rows(Lr, l);
+          if (l < NU) S.clamped[l] = 0;
+        } else {
+          const bool v = l < NU;
+          const double q = v ? S.Qv[NX + l] : 0.0;
+          const double lb = v ? C.u_lb[l] - S.uu[l] : 0.0;
+          const double ub = v ? C.u_ub[l] - S.uu[l] : 0.0;
+          double x = v ? S.kp[l] : 0.0;
+          int clm = 0;
+          ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l);
+          if (ok && v) {
+            const bool c = (clm >> l) & 1;
+            S.kk[l] = -x;
+            S.clamped[l] = c ? 1 : 0;
+            if (c) S.Qv[NX + l] = 0.0;  // BoxFDDP: clamped Qu entries are zeroed
+          }
+        }
+        if (!ok) {
+          failed = true;
+          break;
+        }
+        if (l < NU)
+#pragma unroll
+          for (int j = 0; j < NU; ++j)
+            if (j <= l) S.L[tri(l, j)] = Lr[j];
+      }
+      lds_sync();
+      // ---- phase E: K columns (and k for LLT) ----
+      if (l < NX || (!use_qp && l == NX)) {
+        double col[NU];
+        if (l < NX) {
+#pragma unroll
+          for (int c = 0; c < NU; ++c) col[c] = S.clamped[c] ? 0.0 : S.Q[l * ND + NX + c];
+        } else {
+#pragma unroll
+          for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
+        }
+        chol_solve<NU>(S.L, col);
+        if (l < NX) {
+          double* Kt = d.K + ((long)b * N + t) * NU * NX;
+#pragma unroll
+          for (int c = 0; c < NU; ++c) {
+            S.K[c * NX + l] = col[c];
+            Kt[c * NX + l] = col[c];
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < NU; ++c) S.kk[c] = col[c];
+        }
+      }
+      lds_sync();
+      // ---- phase F: Vxx = sym(Qxx - Qxu K) + preg I (lower triangle, mirrored) ----
+      int badv = 0;
+      for (int e = l; e < NX * (NX + 1) / 2; e += 64) {
+        int i, j;
+        tri_rc(e, i, j);
+        double a1 = 0.0, a2 = 0.0;
+#pragma unroll
+        for (int c = 0; c < NU; ++c) {
+          a1 += S.Q[i * ND + NX + c] * S.K[c * NX + j];
+          a2 += S.Q[j * ND + NX + c] * S.K[c * NX + i];
+        }
+        const double v = S.Q[i * ND + j] - 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
+        S.V[i * NX + j] = v;
+        S.V[j * NX + i] = v;
+        badv |= bad(fabs(v)) ? 1 : 0;
+      }
+      lds_sync();
+      // ---- phase G: Vx, gap terms, expected improvement, k ----
+      double cdg = 0.0, cdq = 0.0, cst = 0.0;
+      if (l < NX) {
+        double vfs = 0.0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
+        double vx = S.Qv[l];
+#pragma unroll
+        for (int c = 0; c < NU; ++c) vx -= S.K[c * NX + l] * S.Qv[NX + c];
+        if (!feas) vx += vfs;
+        badv |= bad(fabs(vx)) ? 1 : 0;
+        if (!feas) {
+          d.w[((long)b * (N + 1) + t) * NX + l] = vfs;
+          cdg -= vx * S.fs[l];
+          cdq += S.fs[l] * vfs;
+        }
+        if (l < NU) {
+          double quk = 0.0;
+#pragma unroll
+          for (int m = 0; m < NU; ++m) quk += S.H[l * NU + m] * S.kk[m];
+          const double qu = S.Qv[NX + l], kl = S.kk[l];
+          cdg += qu * kl;
+          cdq -= kl * quk;
+          cst += qu * qu;
+          d.k[((long)b * N + t) * NU + l] = kl;
+        }
+        S.Vx[l] = vx;  // old Vx is dead after phase B
+      }
+      badv = __any(badv);
+      cdg = wave_sum(cdg);
+      cdq = wave_sum(cdq);
+      cst = wave_sum(cst);
+      if (badv) {
+        failed = true;
+        break;
+      }
+      dg += cdg;
+      dq += cdq;
+      stop += cst;
+      lds_sync();
+    }
+    // ---- retry bookkeeping (SolverFDDP::solve: increaseRegularization) ----
+    if (!failed) break;
+    retries++;
+    preg = fmin(preg * C.reg_inc, C.reg_max);
+    if (preg == C.reg_max) {
+      fail_inst = true;
+      break;
+    }
+    lds_sync();
+  }
+  if (l == 0) {
+    st->preg = preg;
+    st->n_retries += retries;
+    if (fail_inst) {
+      st->bw_ok = 0;
+      st->iter = iter;
+      st->done = 1;
+      st->ok = 0;
+      st->n_backward += retries;
+    } else {
+      st->dg = dg;
+      st->dq = dq;
+      st->stop = stop;
+      st->bw_ok = 1;
+      st->n_backward += retries + 1;
+      st->n_iters += 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // line search: one lane per (instance, step length)
 // ---------------------------------------------------------------------------
 template <int NC, bool FF>
@@ -1017,6 +1561,7 @@ struct ffddp_handle {
   int32_t *out_iters = nullptr, *out_stats = nullptr;
   uint8_t* out_ok = nullptr;
   std::string err;
+  bool bw_wave = true;  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
   // optional per-kernel timing
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -1226,7 +1771,10 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
     }
     {
       ProfScope p(h, s, KC_BACKWARD);
-      hipLaunchKernelGGL((k_backward<FF>), dim3((B + (FF ? 1 : 3)) / (FF ? 2 : 4)), dim3(BW_BLOCK), 0, s, h->dc, d, it);
+      if (h->bw_wave)
+        hipLaunchKernelGGL((k_backward_w<FF>), dim3(B), dim3(64), 0, s, h->dc, d, it);
+      else
+        hipLaunchKernelGGL((k_backward<FF>), dim3((B + (FF ? 1 : 3)) / (FF ? 2 : 4)), dim3(BW_BLOCK), 0, s, h->dc, d, it);
     }
     {
       ProfScope p(h, s, KC_FORWARD);
@@ -1306,6 +1854,14 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   d.N = (int)N;
   d.nx = (int)nx;
   d.rec = rec_size((int)nx);
+  if (d.rec != rec_words((int)nx)) {
+    delete h;
+    return FFDDP_E_INVALID;
+  }
+  {
+    const char* bw = std::getenv("FFDDP_BW");
+    h->bw_wave = !(bw && std::strcmp(bw, "group") == 0);
+  }
   int rc = 0;
   rc |= dalloc(h, &h->dc, 1);
   rc |= dalloc(h, &h->drb, 1);
