@@ -26,17 +26,25 @@
 #include <string>
 #include <vector>
 
-#include "ffddp_node.hpp"
+#include "ffddp_group.hpp"
 
 using namespace ffddp;
 
 namespace {
 
 constexpr int NODE_GROUP = 16;
-constexpr int NODE_BLOCK = 256;
+#ifndef NODE_BLOCK
+#define NODE_BLOCK 64
+#endif
 constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 constexpr int BW_BLOCK = 64;
 constexpr int FW_BLOCK = 64;
+#ifndef NODE_WAVES
+#define NODE_WAVES 2
+#endif
+#ifndef FW_WAVES
+#define FW_WAVES 2
+#endif
 #ifndef BW_WAVES
 #define BW_WAVES 1
 #endif
@@ -62,6 +70,7 @@ struct Dev {
   int* trial_fail;   // [B][T]
   InstState* st;     // [B]
   Primal* prim;      // [B][N+1]  node calc (primal) results for the calcDiff tangents
+  double* link;      // [B][N+1][LK_ALLOC]  per-link world-frame data (rb_links) for the tangents
 };
 
 // ---------------------------------------------------------------------------
@@ -106,6 +115,7 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
 // ---------------------------------------------------------------------------
 struct NodeShared {
   Primal P[NODE_GPB];
+  double lk[NODE_GPB][LK_ALLOC];
   double col[NODE_GPB][14][NDENSE_MAX];  // residual-Jacobian columns, state directions
   double colu[NODE_GPB][7][FFDDP_MAX_NC];  // force rows, inner-control directions
 };
@@ -135,6 +145,12 @@ __global__ __launch_bounds__(64) void k_primal(const DevConsts* __restrict__ Cg,
   Primal P;
   node_primal<NC>(C, mode, surf, y, uin, ref, xreg, xreg + 14, P);
   copy_primal(P, d.prim[node]);
+  {
+    double acc[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) acc[i] = (mode == MODE_TERMINAL_X) ? 0.0 : P.a[i];
+    rb_links(C.rb, y, y + NQ, acc, d.link + node * LK_ALLOC);
+  }
   double* rec = d.rec_buf + node * d.rec;
   // node cost (IAM scaling, FF augmentation terms)
   double cost;
@@ -190,7 +206,7 @@ __global__ __launch_bounds__(64) void k_primal(const DevConsts* __restrict__ Cg,
 
 // calcDiff tangents + Gauss-Newton assembly: 16-lane group per node
 template <int NC, bool FF>
-__global__ __launch_bounds__(NODE_BLOCK) void k_node(const DevConsts* __restrict__ Cg, Dev d,
+__global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE_WAVES))) void k_node(const DevConsts* __restrict__ Cg, Dev d,
                                                       const double* __restrict__ x0,
                                                       const double* __restrict__ node_ref,
                                                       const double* __restrict__ inst_ref,
@@ -217,13 +233,19 @@ __global__ __launch_bounds__(NODE_BLOCK) void k_node(const DevConsts* __restrict
     double* dst = reinterpret_cast<double*>(&P);
     constexpr int nw = sizeof(Primal) / sizeof(double);
     for (int e = lane; e < nw; e += NODE_GROUP) dst[e] = src[e];
+    const double* ls = d.link + node * LK_ALLOC;
+    for (int e = lane; e < LK_WORDS; e += NODE_GROUP) S.lk[grp][e] = ls[e];
   }
   __syncthreads();
   const bool need_u = mode != MODE_TERMINAL_X;
   double da[NQ], dlam[3], col[NDENSE_MAX];
   double dau[NQ], dlamu[3];
   if (active && lane < 14) {
+#ifdef FFDDP_DUAL_TANGENT
     node_tangent_state<NC>(C, mode, surf, y, ref, P, lane, da, dlam, col);
+#else
+    node_tangent_state_an<NC>(C, mode, surf, S.lk[grp], P, lane, da, dlam, col);
+#endif
     for (int r = 0; r < 12 + nc; ++r) S.col[grp][lane][r] = col[r];
   }
   if (active && lane < 7 && need_u) {
@@ -1418,6 +1440,132 @@ __global__ __launch_bounds__(FW_BLOCK) void k_forward(const DevConsts* __restric
 }
 
 // ---------------------------------------------------------------------------
+// line search with an 8-lane group per (instance, step length): the rollout
+// of one trial is still sequential over the nodes, but each node calc runs
+// joint-parallel (node_calc_g8), which shortens the dependent chain that
+// bounds this kernel.  Lane i < 7 carries joint i of x (q_i, v_i, FF tau_i).
+// ---------------------------------------------------------------------------
+template <int NC, bool FF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) void k_forward_g8(const DevConsts* __restrict__ Cg, Dev d,
+                                                   const double* __restrict__ x0,
+                                                   const double* __restrict__ node_ref,
+                                                   const double* __restrict__ inst_ref,
+                                                   const uint8_t* __restrict__ surface) {
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  constexpr int nx = FF ? 21 : 14;
+  const long gid = (blockIdx.x * (long)blockDim.x + threadIdx.x) / G8;
+  const int li = g8_lane();
+  const bool J = li < NQ;
+  const int ji = J ? li : 0;
+  const int b = (int)(gid / NTRIALS), tr = (int)(gid % NTRIALS);
+  if (b >= d.B) return;
+  const InstState* st = d.st + b;
+  if (st->done) return;
+  const double alpha = C.alphas[tr];
+  const bool feas = st->is_feasible != 0;
+  const bool gap = !(feas || alpha == 1.0);
+  const bool surf = surface[b] != 0;
+  const double* xreg = inst_ref + (long)b * 21;
+  const double* yref = x0 + (long)b * nx;
+  const double xq = xreg[ji], xv = xreg[7 + ji], tref = xreg[14 + ji];
+  // predicted state (lane-local joint components)
+  double hq = J ? x0[(long)b * nx + ji] : 0.0;
+  double hv = J ? x0[(long)b * nx + 7 + ji] : 0.0;
+  double ht = (FF && J) ? x0[(long)b * nx + 14 + ji] : 0.0;
+  double cost = 0.0, dvp = 0.0;
+  bool fail = false;
+  double* xtr = d.xs_try + ((long)b * NTRIALS + tr) * (N + 1) * nx;
+  double* utr = d.us_try + ((long)b * NTRIALS + tr) * N * NU;
+  for (int t = 0; t <= N; ++t) {
+    const double* xs_t = d.xs + ((long)b * (N + 1) + t) * nx;
+    const double* fs_t = d.fs + ((long)b * (N + 1) + t) * nx;
+    double xq_t = hq, xv_t = hv, xt_t = ht;
+    double sq = 0.0, sv = 0.0, stt = 0.0;
+    if (J) {
+      sq = xs_t[ji];
+      sv = xs_t[7 + ji];
+      if (FF) stt = xs_t[14 + ji];
+      if (gap) {
+        xq_t = hq + fs_t[ji] * (alpha - 1.0);
+        xv_t = hv + fs_t[7 + ji] * (alpha - 1.0);
+        if (FF) xt_t = ht + fs_t[14 + ji] * (alpha - 1.0);
+      }
+      if (!feas) {
+        const double* w_t = d.w + ((long)b * (N + 1) + t) * nx;
+        dvp -= w_t[ji] * (sq - xq_t) + w_t[7 + ji] * (sv - xv_t) + (FF ? w_t[14 + ji] * (stt - xt_t) : 0.0);
+      }
+      xtr[(long)t * nx + ji] = xq_t;
+      xtr[(long)t * nx + 7 + ji] = xv_t;
+      if (FF) xtr[(long)t * nx + 14 + ji] = xt_t;
+    }
+    const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
+    if (t < N) {
+      // u_i = us_i - alpha k_i - K_i (x - xs)
+      double u = 0.0;
+      {
+        const double* K_t = d.K + ((long)b * N + t) * NU * nx + (long)ji * nx;
+        double acc = J ? d.us[((long)b * N + t) * NU + ji] - d.k[((long)b * N + t) * NU + ji] * alpha : 0.0;
+        const double dq = xq_t - sq, dv = xv_t - sv, dtt = xt_t - stt;
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) {
+          const double dqm = g8_get(dq, m), dvm = g8_get(dv, m);
+          acc -= (J ? K_t[m] : 0.0) * dqm;
+          acc -= (J ? K_t[7 + m] : 0.0) * dvm;
+          if (FF) acc -= (J ? K_t[14 + m] : 0.0) * g8_get(dtt, m);
+        }
+        // crocoddyl order: sum over x components 0..nx-1 (q then v then tau); rounding-level difference only
+        if (C.use_box) acc = fmin(fmax(acc, C.u_lb[ji]), C.u_ub[ji]);
+        u = acc;
+        if (J) utr[(long)t * NU + ji] = u;
+      }
+      double qn, vn, cp, lam[3];
+      const double uin = FF ? xt_t : u;
+      node_calc_g8<NC>(C, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam);
+      double c = C.dt * cp;
+      double tn = 0.0;
+      if (FF) {
+        tn = C.alpha * xt_t + C.beta * u;
+        if (J) {
+          const double e1 = xq_t - yref[ji], e2 = xv_t - yref[7 + ji], e3 = xt_t - yref[14 + ji];
+          c += 0.5 * C.w_y * (C.Wy2[ji] * e1 * e1 + C.Wy2[7 + ji] * e2 * e2 + C.Wy2[14 + ji] * e3 * e3);
+          c += 0.5 * C.w_w * u * u;
+          const double ov = fabs(u) - C.ws_lim[ji];
+          const double oo = ov > 0.0 ? ov : 0.0;
+          c += C.w_ws * (0.5 * oo * oo);
+        }
+      }
+      cost += g8_sum(c);
+      const int xbad = g8_or((J && (bad(fabs(qn)) || bad(fabs(vn)) || (FF && bad(fabs(tn))))) ? 1 : 0);
+      if (bad(cost) || xbad) {
+        fail = true;
+        break;
+      }
+      hq = qn;
+      hv = vn;
+      ht = tn;
+    } else {
+      double qn, vn, cp, lam[3];
+      const int mode = FF ? MODE_TERMINAL_U : MODE_TERMINAL_X;
+      node_calc_g8<NC>(C, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam);
+      double c = FF ? C.dt * cp : cp;
+      if (FF && J) {
+        const double e1 = xq_t - yref[ji], e2 = xv_t - yref[7 + ji], e3 = xt_t - yref[14 + ji];
+        c += 0.5 * C.w_y * (C.Wy2[ji] * e1 * e1 + C.Wy2[7 + ji] * e2 * e2 + C.Wy2[14 + ji] * e3 * e3);
+      }
+      cost += g8_sum(c);
+      if (bad(cost)) fail = true;
+    }
+  }
+  const double dv = g8_sum(dvp);
+  if (li == 0) {
+    d.trial[((long)b * NTRIALS + tr) * 2 + 0] = cost;
+    d.trial[((long)b * NTRIALS + tr) * 2 + 1] = dv;
+    d.trial_fail[(long)b * NTRIALS + tr] = fail ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // acceptance / regularisation / stopping: one lane per instance
 // ---------------------------------------------------------------------------
 __global__ void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter) {
@@ -1561,7 +1709,8 @@ struct ffddp_handle {
   int32_t *out_iters = nullptr, *out_stats = nullptr;
   uint8_t* out_ok = nullptr;
   std::string err;
-  bool bw_wave = true;  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
+  bool bw_wave = true;
+  bool fw_group = false;  // 8-lane joint-parallel line search (FFDDP_FW=group); default one lane per trial  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
   // optional per-kernel timing
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -1714,7 +1863,7 @@ template <class T> int dalloc(ffddp_handle* h, T** p, size_t n) {
 }
 
 void free_all(ffddp_handle* h) {
-  void* ps[] = {h->dc, h->drb, h->d.prim, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
+  void* ps[] = {h->dc, h->drb, h->d.prim, h->d.link, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
                 h->d.us_try, h->d.trial, h->d.trial_fail, h->d.st, h->in_x0, h->in_nref, h->in_iref, h->in_xs,
                 h->in_us, h->in_surf, h->out_xs, h->out_us, h->out_K, h->out_cost, h->out_fn, h->out_iters,
                 h->out_stats, h->out_ok};
@@ -1778,7 +1927,11 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
     }
     {
       ProfScope p(h, s, KC_FORWARD);
-      hipLaunchKernelGGL((k_forward<NC, FF>), dim3(fw_blocks), dim3(FW_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf);
+      if (h->fw_group)
+        hipLaunchKernelGGL((k_forward_g8<NC, FF>), dim3((int)(((long)B * NTRIALS * G8 + 63) / 64)), dim3(64), 0, s, h->dc,
+                           d, x0, nref, iref, surf);
+      else
+        hipLaunchKernelGGL((k_forward<NC, FF>), dim3(fw_blocks), dim3(FW_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf);
     }
     {
       ProfScope p(h, s, KC_ACCEPT);
@@ -1861,6 +2014,8 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   {
     const char* bw = std::getenv("FFDDP_BW");
     h->bw_wave = !(bw && std::strcmp(bw, "group") == 0);
+    const char* fw = std::getenv("FFDDP_FW");
+    h->fw_group = fw && std::strcmp(fw, "group") == 0;
   }
   int rc = 0;
   rc |= dalloc(h, &h->dc, 1);
@@ -1872,6 +2027,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   rc |= dalloc(h, &d.K, (size_t)B * N * NU * nx);
   rc |= dalloc(h, &d.k, (size_t)B * N * NU);
   rc |= dalloc(h, &d.w, (size_t)B * (N + 1) * nx);
+  rc |= dalloc(h, &d.link, (size_t)B * (N + 1) * LK_ALLOC);
   rc |= dalloc(h, &d.xs_try, (size_t)B * NTRIALS * (N + 1) * nx);
   rc |= dalloc(h, &d.us_try, (size_t)B * NTRIALS * N * NU);
   rc |= dalloc(h, &d.trial, (size_t)B * NTRIALS * 2);

@@ -574,6 +574,287 @@ FFD_HD void node_tangent_state(const DevConsts& C, int mode, bool surface, const
   }
 }
 
+// ---------------------------------------------------------------------------
+// Closed-form state tangent (replaces the forward-mode dual pass above in the
+// calcDiff kernel).  World-frame spatial algebra, S_j = (o_j x z_j, z_j):
+//   q_j : every link k >= j rotates about S_j, so
+//         dV_k = S_j x (V_k - V_{j-1}),
+//         dA_k = S_j x (A_k - A_{j-1}) + cV x (V_k - V_{j-1}),  cV = -S_j x V_{j-1}
+//         dF_k = S_j x* F_k + I_k Y_k + T x* H_k + V_k x* (I_k T),
+//                Y_k = cA + cV x (V_k - V_{j-1}), cA = -S_j x (A_{j-1} - G), T = cV
+//   v_j : dV_k = S_j, dA_k = S_j x (V_k - 2 V_{j-1}),
+//         dF_k = I_k Y_k + T x* H_k + V_k x* (I_k T),
+//                Y_k = -S_j x V_{j-1} + S_j x (V_k - V_{j-1}), T = S_j
+// (F = I (A - G) + V x* (I V), H = I V; x = motion cross, x* = force cross),
+// then d tau_i = dS_i . Ftot_i + S_i . dFtot_i over the suffix sums (the
+// contact force is a world-fixed vector at the moving EE point).  Same
+// outputs as node_tangent_state: da, dlam, residual-Jacobian column.
+// ---------------------------------------------------------------------------
+FFD_HD void sp_mcross(const double* sv, const double* sw, const double* xv, const double* xw, double* ov, double* ow) {
+  // (sw x xv + sv x xw, sw x xw)
+  ov[0] = sw[1] * xv[2] - sw[2] * xv[1] + sv[1] * xw[2] - sv[2] * xw[1];
+  ov[1] = sw[2] * xv[0] - sw[0] * xv[2] + sv[2] * xw[0] - sv[0] * xw[2];
+  ov[2] = sw[0] * xv[1] - sw[1] * xv[0] + sv[0] * xw[1] - sv[1] * xw[0];
+  ow[0] = sw[1] * xw[2] - sw[2] * xw[1];
+  ow[1] = sw[2] * xw[0] - sw[0] * xw[2];
+  ow[2] = sw[0] * xw[1] - sw[1] * xw[0];
+}
+FFD_HD void sp_fcross(const double* xv, const double* xw, const double* f, const double* n, double* of, double* on) {
+  // (xw x f, xw x n + xv x f)
+  of[0] = xw[1] * f[2] - xw[2] * f[1];
+  of[1] = xw[2] * f[0] - xw[0] * f[2];
+  of[2] = xw[0] * f[1] - xw[1] * f[0];
+  on[0] = xw[1] * n[2] - xw[2] * n[1] + xv[1] * f[2] - xv[2] * f[1];
+  on[1] = xw[2] * n[0] - xw[0] * n[2] + xv[2] * f[0] - xv[0] * f[2];
+  on[2] = xw[0] * n[1] - xw[1] * n[0] + xv[0] * f[1] - xv[1] * f[0];
+}
+FFD_HD void sp_imul(double m, const double* h, const double* IO, const double* xv, const double* xw, double* of,
+                    double* on) {
+  // (m xv - h x xw, h x xv + I_O xw)
+  of[0] = m * xv[0] - (h[1] * xw[2] - h[2] * xw[1]);
+  of[1] = m * xv[1] - (h[2] * xw[0] - h[0] * xw[2]);
+  of[2] = m * xv[2] - (h[0] * xw[1] - h[1] * xw[0]);
+  on[0] = (h[1] * xv[2] - h[2] * xv[1]) + IO[0] * xw[0] + IO[1] * xw[1] + IO[2] * xw[2];
+  on[1] = (h[2] * xv[0] - h[0] * xv[2]) + IO[1] * xw[0] + IO[3] * xw[1] + IO[4] * xw[2];
+  on[2] = (h[0] * xv[1] - h[1] * xv[0]) + IO[2] * xw[0] + IO[4] * xw[1] + IO[5] * xw[2];
+}
+
+template <int NC>
+FFD_HD void node_tangent_state_an(const DevConsts& C, int mode, bool surface, const double* LK, const Primal& P,
+                                  int dir, double* da, double* dlam, double* col) {
+  constexpr int nc = NC;
+  const bool with_dyn = mode != MODE_TERMINAL_X;
+  const bool isq = dir < NQ;
+  const int j = isq ? dir : dir - NQ;
+  const double* Lj = LK + j * LK_STRIDE;
+  const double* Lp = LK + (j > 0 ? j - 1 : 0) * LK_STRIDE;
+  const double pz = j > 0 ? 1.0 : 0.0;
+  double Sv[3], Sz[3], oj[3], Vpv[3], Vpw[3], Apv[3], Apw[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    Sv[k] = Lj[LK_SV + k];
+    Sz[k] = Lj[LK_Z + k];
+    oj[k] = Lj[LK_O + k];
+    Vpv[k] = pz * Lp[LK_VO + k];
+    Vpw[k] = pz * Lp[LK_W + k];
+    Apv[k] = pz * Lp[LK_AO + k] - C.rb.gravity[k];  // A_{j-1} - G
+    Apw[k] = pz * Lp[LK_AL + k];
+  }
+  const double* E = LK + LK_EE;
+  const double pee[3] = {E[0], E[1], E[2]}, vp[3] = {E[3], E[4], E[5]}, wee[3] = {E[6], E[7], E[8]};
+  const double* L6 = LK + (NQ - 1) * LK_STRIDE;
+  const double qs = isq ? 1.0 : 0.0;
+  // cV = -S_j x V_{j-1} ; T = q ? cV : S_j ; Cc = q ? -S_j x (A_{j-1} - G) : cV
+  double cVv[3], cVw[3], cAv[3], cAw[3];
+  sp_mcross(Sv, Sz, Vpv, Vpw, cVv, cVw);
+  sp_mcross(Sv, Sz, Apv, Apw, cAv, cAw);
+  double Tv[3], Tw[3], Ccv[3], Ccw[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    cVv[k] = -cVv[k];
+    cVw[k] = -cVw[k];
+    Tv[k] = isq ? cVv[k] : Sv[k];
+    Tw[k] = isq ? cVw[k] : Sz[k];
+    Ccv[k] = isq ? -cAv[k] : cVv[k];
+    Ccw[k] = isq ? -cAw[k] : cVw[k];
+  }
+  // Dm = q ? cV : S_j  (multiplies (V_k - V_{j-1}) in Y_k); for v_j Y_k = cV + S_j x (V_k - V_{j-1})
+  // ---- end-effector tangents ----
+  double dpee[3] = {0, 0, 0};
+  {
+    const double r[3] = {pee[0] - oj[0], pee[1] - oj[1], pee[2] - oj[2]};
+    dpee[0] = qs * (Sz[1] * r[2] - Sz[2] * r[1]);
+    dpee[1] = qs * (Sz[2] * r[0] - Sz[0] * r[2]);
+    dpee[2] = qs * (Sz[0] * r[1] - Sz[1] * r[0]);
+  }
+  double d6v[3], d6w[3];  // dV_6
+  double dA6v[3], dA6w[3];
+  {
+    const double D6v[3] = {L6[LK_VO] - Vpv[0], L6[LK_VO + 1] - Vpv[1], L6[LK_VO + 2] - Vpv[2]};
+    const double D6w[3] = {L6[LK_W] - Vpw[0], L6[LK_W + 1] - Vpw[1], L6[LK_W + 2] - Vpw[2]};
+    double t1v[3], t1w[3];
+    sp_mcross(Sv, Sz, D6v, D6w, t1v, t1w);  // S_j x (V_6 - V_{j-1})
+    // A_6 - A_{j-1}  (gravity cancels)
+    const double DAv[3] = {L6[LK_AO] - pz * Lp[LK_AO], L6[LK_AO + 1] - pz * Lp[LK_AO + 1], L6[LK_AO + 2] - pz * Lp[LK_AO + 2]};
+    const double DAw[3] = {L6[LK_AL] - Apw[0], L6[LK_AL + 1] - Apw[1], L6[LK_AL + 2] - Apw[2]};
+    double t2v[3], t2w[3], t3v[3], t3w[3];
+    sp_mcross(Sv, Sz, DAv, DAw, t2v, t2w);   // S_j x (A_6 - A_{j-1})
+    sp_mcross(cVv, cVw, D6v, D6w, t3v, t3w);  // cV x (V_6 - V_{j-1})
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      d6v[k] = isq ? t1v[k] : Sv[k];
+      d6w[k] = isq ? t1w[k] : Sz[k];
+      // q: S x (A6 - Ap) + cV x (V6 - Vp) ; v: S x (V6 - Vp) + cV  x ... = S x (V6 - 2 Vp) = t1 + cV
+      dA6v[k] = isq ? t2v[k] + t3v[k] : t1v[k] + cVv[k];
+      dA6w[k] = isq ? t2w[k] + t3w[k] : t1w[k] + cVw[k];
+    }
+  }
+  double dvp[3], dap[3];
+  {
+    double c1[3], c2[3];
+    const double* w6 = wee;
+    // dvp = dvO + dw x p + w x dp
+    c1[0] = d6w[1] * pee[2] - d6w[2] * pee[1];
+    c1[1] = d6w[2] * pee[0] - d6w[0] * pee[2];
+    c1[2] = d6w[0] * pee[1] - d6w[1] * pee[0];
+    c2[0] = w6[1] * dpee[2] - w6[2] * dpee[1];
+    c2[1] = w6[2] * dpee[0] - w6[0] * dpee[2];
+    c2[2] = w6[0] * dpee[1] - w6[1] * dpee[0];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dvp[k] = d6v[k] + c1[k] + c2[k];
+    // dap = daO + dal x p + al x dp + dw x vp + w x dvp
+    const double al6[3] = {L6[LK_AL], L6[LK_AL + 1], L6[LK_AL + 2]};
+    double c3[3], c4[3], c5[3], c6[3];
+    c3[0] = dA6w[1] * pee[2] - dA6w[2] * pee[1];
+    c3[1] = dA6w[2] * pee[0] - dA6w[0] * pee[2];
+    c3[2] = dA6w[0] * pee[1] - dA6w[1] * pee[0];
+    c4[0] = al6[1] * dpee[2] - al6[2] * dpee[1];
+    c4[1] = al6[2] * dpee[0] - al6[0] * dpee[2];
+    c4[2] = al6[0] * dpee[1] - al6[1] * dpee[0];
+    c5[0] = d6w[1] * vp[2] - d6w[2] * vp[1];
+    c5[1] = d6w[2] * vp[0] - d6w[0] * vp[2];
+    c5[2] = d6w[0] * vp[1] - d6w[1] * vp[0];
+    c6[0] = w6[1] * dvp[2] - w6[2] * dvp[1];
+    c6[1] = w6[2] * dvp[0] - w6[0] * dvp[2];
+    c6[2] = w6[0] * dvp[1] - w6[1] * dvp[0];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dap[k] = dA6v[k] + c3[k] + c4[k] + c5[k] + c6[k];
+  }
+  // ---- residual-Jacobian column ----
+  {
+    double wl[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) wl[i] = qs * (P.Ree[0 * 3 + i] * Sz[0] + P.Ree[1 * 3 + i] * Sz[1] + P.Ree[2 * 3 + i] * Sz[2]);
+    col[0] = dpee[0];
+    col[1] = dpee[1];
+    col[2] = dpee[2];
+    double Jlog[9];
+    jlog3(P.r_rot, P.th_rot, Jlog);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) col[3 + i] = Jlog[3 * i + 0] * wl[0] + Jlog[3 * i + 1] * wl[1] + Jlog[3 * i + 2] * wl[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      col[6 + i] = dvp[i];
+      col[9 + i] = d6w[i];
+    }
+#pragma unroll
+    for (int r = 0; r < nc; ++r) col[12 + r] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) da[i] = 0.0;
+  dlam[0] = dlam[1] = dlam[2] = 0.0;
+  if (!with_dyn) return;
+  // ---- d tau = d RNEA(q, v, a, fext = lambda) / d x_j at fixed a, lambda ----
+  double lw[3] = {0, 0, 0};
+  if (surface) force_world<NC>(P.lam, lw);
+  double Fe[3], dFe[3];  // moment parts of Fext and dFext (linear parts: lw and 0)
+  Fe[0] = pee[1] * lw[2] - pee[2] * lw[1];
+  Fe[1] = pee[2] * lw[0] - pee[0] * lw[2];
+  Fe[2] = pee[0] * lw[1] - pee[1] * lw[0];
+  dFe[0] = dpee[1] * lw[2] - dpee[2] * lw[1];
+  dFe[1] = dpee[2] * lw[0] - dpee[0] * lw[2];
+  dFe[2] = dpee[0] * lw[1] - dpee[1] * lw[0];
+  double FSf[3] = {0, 0, 0}, FSn[3] = {0, 0, 0}, dSf[3] = {0, 0, 0}, dSn[3] = {0, 0, 0};
+  double r1[NQ];
+#pragma unroll
+  for (int k = NQ - 1; k >= 0; --k) {
+    const double* Lk = LK + k * LK_STRIDE;
+    const double* Vk = Lk + LK_VO;
+    const double* Wk = Lk + LK_W;
+    const double* Fk = Lk + LK_F;
+    const double* Nk = Lk + LK_N;
+    const double* Hl = Lk + LK_HL;
+    const double* Ha = Lk + LK_HA;
+    const double m = Lk[LK_M];
+    const double* h = Lk + LK_H;
+    const double* IO = Lk + LK_IO;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      FSf[e] += Fk[e];
+      FSn[e] += Nk[e];
+    }
+    const double mk = (k >= j) ? 1.0 : 0.0;
+    // Y = Cc + Dm x (V_k - V_{j-1}),  Dm = q ? cV : S_j
+    const double Dv[3] = {Vk[0] - Vpv[0], Vk[1] - Vpv[1], Vk[2] - Vpv[2]};
+    const double Dw[3] = {Wk[0] - Vpw[0], Wk[1] - Vpw[1], Wk[2] - Vpw[2]};
+    double Dmv[3], Dmw[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      Dmv[e] = isq ? cVv[e] : Sv[e];
+      Dmw[e] = isq ? cVw[e] : Sz[e];
+    }
+    double Yv[3], Yw[3];
+    sp_mcross(Dmv, Dmw, Dv, Dw, Yv, Yw);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      Yv[e] += Ccv[e];
+      Yw[e] += Ccw[e];
+    }
+    double a1f[3], a1n[3], a2f[3], a2n[3], a3f[3], a3n[3], ITf[3], ITn[3], a4f[3], a4n[3];
+    sp_imul(m, h, IO, Yv, Yw, a1f, a1n);      // I_k Y
+    sp_fcross(Tv, Tw, Hl, Ha, a2f, a2n);      // T x* H_k
+    sp_imul(m, h, IO, Tv, Tw, ITf, ITn);      // I_k T
+    sp_fcross(Vk, Wk, ITf, ITn, a3f, a3n);    // V_k x* (I_k T)
+    sp_fcross(Sv, Sz, Fk, Nk, a4f, a4n);      // S_j x* F_k   (q only)
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      dSf[e] += mk * (a1f[e] + a2f[e] + a3f[e] + qs * a4f[e]);
+      dSn[e] += mk * (a1n[e] + a2n[e] + a3n[e] + qs * a4n[e]);
+    }
+    // dS_k = S_j x S_k for q_j, k > j
+    const double* Svk = Lk + LK_SV;
+    const double* Szk = Lk + LK_Z;
+    double dSv[3], dSw[3];
+    sp_mcross(Sv, Sz, Svk, Szk, dSv, dSw);
+    const double ms = (isq && k > j) ? 1.0 : 0.0;
+    const double Ftf[3] = {FSf[0] - lw[0], FSf[1] - lw[1], FSf[2] - lw[2]};
+    const double Ftn[3] = {FSn[0] - Fe[0], FSn[1] - Fe[1], FSn[2] - Fe[2]};
+    const double dFtn[3] = {dSn[0] - dFe[0], dSn[1] - dFe[1], dSn[2] - dFe[2]};
+    const double dtau = ms * (dSv[0] * Ftf[0] + dSv[1] * Ftf[1] + dSv[2] * Ftf[2] + dSw[0] * Ftn[0] + dSw[1] * Ftn[1] +
+                              dSw[2] * Ftn[2]) +
+                        (Svk[0] * dSf[0] + Svk[1] * dSf[1] + Svk[2] * dSf[2] + Szk[0] * dFtn[0] + Szk[1] * dFtn[1] +
+                         Szk[2] * dFtn[2]);
+    r1[k] = -dtau;
+  }
+  if (!surface) {
+    chol_solve<NQ>(P.L, r1);
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) da[i] = r1[i];
+    return;
+  }
+  // dh = d (classical acc + Kp (p - p*) + Kd v_p) / d x_j
+  constexpr int c0 = NC == 1 ? 2 : 0;
+  double dh[3];
+#pragma unroll
+  for (int r = 0; r < nc; ++r) dh[r] = dap[c0 + r] + C.Kp * dpee[c0 + r] + C.Kd * dvp[c0 + r];
+  double mr[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) mr[i] = r1[i];
+  chol_solve<NQ>(P.L, mr);
+  double yl[3];
+#pragma unroll
+  for (int r = 0; r < nc; ++r) {
+    double acc = dh[r];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) acc += P.Jc[r][i] * mr[i];
+    yl[r] = acc;
+  }
+  chol_solve<NC>(P.Ls, yl);
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    double acc = r1[i];
+#pragma unroll
+    for (int r = 0; r < nc; ++r) acc -= P.Jc[r][i] * yl[r];
+    da[i] = acc;
+  }
+  chol_solve<NQ>(P.L, da);
+#pragma unroll
+  for (int r = 0; r < nc; ++r) {
+    dlam[r] = -yl[r];
+    col[12 + r] = (mode == MODE_TERMINAL_X) ? 0.0 : dlam[r];
+  }
+}
+
 // control direction k in [0,7): dg = -e_k, dh = 0
 template <int NC>
 FFD_HD void node_tangent_control(const DevConsts& C, bool surface, const Primal& P, int k, double* da, double* dlam) {

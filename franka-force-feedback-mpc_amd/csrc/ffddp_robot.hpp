@@ -168,6 +168,104 @@ FFD_HD void rb_pass(const ffddp_robot& rb, const T* q, const T* v, const double*
   }
 }
 
+// ---------------------------------------------------------------------------
+// Per-link world-frame data at (q, v, qdd = a) for the closed-form tangents
+// of the calcDiff kernel (layout LK_*; double only).  Per link k:
+//   S = (o x z, z), o, V = (vO, w), A = (aO, al) (qdd = a), F = I (A - G) +
+//   V x* (I V) (link force, no contact), H = I V, tuple (m, h = m c, I_O);
+// then the EE: p, v_p (LWA), w, classical acceleration a_p (qdd = a).
+// ---------------------------------------------------------------------------
+constexpr int LK_SV = 0, LK_Z = 3, LK_O = 6, LK_VO = 9, LK_W = 12, LK_AO = 15, LK_AL = 18, LK_F = 21, LK_N = 24,
+              LK_HL = 27, LK_HA = 30, LK_M = 33, LK_H = 34, LK_IO = 37, LK_STRIDE = 43;
+constexpr int LK_EE = FFDDP_NQ * LK_STRIDE;  // pee(3) vp(3) w(3) ap(3)
+constexpr int LK_WORDS = LK_EE + 12;         // 313
+constexpr int LK_ALLOC = 320;
+
+FFD_HD void rb_links(const ffddp_robot& rb, const double* q, const double* v, const double* a, double* lk) {
+  M3<double> Rprev = m3eye<double>();
+  V3<double> oprev = v3zero<double>();
+  V3<double> vO = v3zero<double>(), w = v3zero<double>(), aO = v3zero<double>(), al = v3zero<double>();
+  const V3<double> g = v3c<double>(rb.gravity);
+#pragma unroll
+  for (int i = 0; i < FFDDP_NQ; ++i) {
+    double* L = lk + i * LK_STRIDE;
+    const V3<double> o = oprev + mulc_v(Rprev, rb.joint_p[i]);
+    const M3<double> Rp = mulc(Rprev, rb.joint_R[i]);
+    double s, c;
+    sincos_(q[i], s, c);
+    M3<double> R;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      R.m[3 * r + 0] = c * Rp.m[3 * r + 0] + s * Rp.m[3 * r + 1];
+      R.m[3 * r + 1] = c * Rp.m[3 * r + 1] - s * Rp.m[3 * r + 0];
+      R.m[3 * r + 2] = Rp.m[3 * r + 2];
+    }
+    const V3<double> z = {R.m[2], R.m[5], R.m[8]};
+    const V3<double> Sv = cross(o, z);
+    const V3<double> Svq = v[i] * Sv, zq = v[i] * z;
+    vO = vO + Svq;
+    w = w + zq;
+    aO = aO + scale(Sv, a[i]) + (cross(w, Svq) + cross(vO, zq));
+    al = al + scale(z, a[i]) + cross(w, zq);
+    // inertia tuple about the world origin
+    const double m = rb.mass[i];
+    const V3<double> cw = o + mulc_v(R, rb.com[i]);
+    double IcR[9], Iw[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc)
+        IcR[3 * r + cc] = rb.inertia[i][3 * r + 0] * R.m[3 * cc + 0] + rb.inertia[i][3 * r + 1] * R.m[3 * cc + 1] +
+                          rb.inertia[i][3 * r + 2] * R.m[3 * cc + 2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc)
+        Iw[3 * r + cc] = R.m[3 * r + 0] * IcR[0 * 3 + cc] + R.m[3 * r + 1] * IcR[1 * 3 + cc] + R.m[3 * r + 2] * IcR[2 * 3 + cc];
+    const double c2 = dot(cw, cw);
+    const V3<double> h = scale(cw, m);
+    const double IO[6] = {Iw[0] + m * (c2 - cw.x * cw.x), Iw[1] - m * cw.x * cw.y, Iw[2] - m * cw.x * cw.z,
+                          Iw[4] + m * (c2 - cw.y * cw.y), Iw[5] - m * cw.y * cw.z, Iw[8] + m * (c2 - cw.z * cw.z)};
+    auto IOmul = [&](V3<double> x) -> V3<double> {
+      return {IO[0] * x.x + IO[1] * x.y + IO[2] * x.z, IO[1] * x.x + IO[3] * x.y + IO[4] * x.z,
+              IO[2] * x.x + IO[4] * x.y + IO[5] * x.z};
+    };
+    // H = I V ; F = I (A - G) + V x* H
+    const V3<double> hl = scale(vO, m) - cross(h, w);
+    const V3<double> ha = cross(h, vO) + IOmul(w);
+    const V3<double> ag = aO - g;
+    const V3<double> f1 = scale(ag, m) - cross(h, al);
+    const V3<double> n1 = cross(h, ag) + IOmul(al);
+    const V3<double> f = f1 + cross(w, hl);
+    const V3<double> n = n1 + cross(w, ha) + cross(vO, hl);
+    const V3<double> vals[11] = {Sv, z, o, vO, w, aO, al, f, n, hl, ha};
+#pragma unroll
+    for (int e = 0; e < 11; ++e) {
+      L[3 * e + 0] = vals[e].x;
+      L[3 * e + 1] = vals[e].y;
+      L[3 * e + 2] = vals[e].z;
+    }
+    L[LK_M] = m;
+    L[LK_H + 0] = h.x;
+    L[LK_H + 1] = h.y;
+    L[LK_H + 2] = h.z;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) L[LK_IO + e] = IO[e];
+    Rprev = R;
+    oprev = o;
+  }
+  const V3<double> pee = oprev + mulc_v(Rprev, rb.ee_p);
+  const V3<double> vp = vO + cross(w, pee);
+  const V3<double> ap = aO + cross(al, pee) + cross(w, vp);
+  const V3<double> ee[4] = {pee, vp, w, ap};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    lk[LK_EE + 3 * e + 0] = ee[e].x;
+    lk[LK_EE + 3 * e + 1] = ee[e].y;
+    lk[LK_EE + 3 * e + 2] = ee[e].z;
+  }
+}
+
 // gravity torque rnea(q, 0, 0) (crocoddyl_classical.py:447-451)
 FFD_HD void gravity_torque(const ffddp_robot& rb, const double* q, double* tau) {
   double zero[FFDDP_NQ] = {0, 0, 0, 0, 0, 0, 0};
