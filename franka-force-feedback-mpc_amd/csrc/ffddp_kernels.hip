@@ -894,6 +894,18 @@ template <bool FF> __device__ __forceinline__ int itilde(int c, double dt, doubl
   return 1;
 }
 
+// branch-free form of itilde: two (row, coef) terms, coef 0 where absent (row kept in range)
+template <bool FF>
+__device__ __forceinline__ void itilde2(int c, double dt, double alpha, double beta, int& r0, double& a0, int& r1,
+                                        double& a1) {
+  const bool lo = c < 14;
+  a0 = lo ? 1.0 : (FF ? (c < 21 ? alpha : beta) : 0.0);
+  r0 = lo ? c : (FF ? (c < 21 ? c : c - 7) : 0);
+  const bool vel = c >= 7 && c < 14;
+  a1 = vel ? dt : 0.0;
+  r1 = vel ? c - 7 : 0;
+}
+
 // A^[m][c] = d a_m / d dir_c (record rows 0..20; FF w-columns 21..27 are zero)
 template <bool FF> __device__ __forceinline__ double ahat(const double* Ar, int m, int c) {
   return (FF && c >= 21) ? 0.0 : Ar[c * 7 + m];
@@ -1079,6 +1091,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
   int retries = 0;
   bool fail_inst = false;
   double dg = 0.0, dq = 0.0, stop = 0.0;
+  // this lane's lower-triangle entries of Q (phase C) and V (phase F), fixed for the whole pass
+  constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 63) / 64;
+  constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 63) / 64;
+  int qrc[NQL], vij[NVL];
+#pragma unroll
+  for (int k = 0; k < NQL; ++k) {
+    int r = 0, c = 0;
+    if (l + 64 * k < NQE) tri_rc(l + 64 * k, r, c);
+    qrc[k] = (r << 8) | c;
+  }
+#pragma unroll
+  for (int k = 0; k < NVL; ++k) {
+    int i = 0, j = 0;
+    if (l + 64 * k < NVE) tri_rc(l + 64 * k, i, j);
+    vij[k] = (i << 8) | j;
+  }
   for (;;) {
     dg = dq = stop = 0.0;
     bool failed = false;
@@ -1145,74 +1173,82 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
       }
       lds_sync();
       const double* Ar = S.R + rec_off_A();
-      // ---- phase A: W = V D, Y = D' V D, z = D' Vx ----
-      for (int e = l; e < NX * NU + NU * NU + NU; e += 64) {
+      // ---- phase A: W = V D (NX x 7), Y = D' V D (7 x 7), z = D' Vx ----
+#pragma unroll
+      for (int k = 0; k < (NX * NU + 63) / 64; ++k) {
+        const int e = l + 64 * k;
         if (e < NX * NU) {
-          const int i = e / NU, m = e % NU;
+          const int i = e / NU, m = e - (e / NU) * NU;
           S.W[e] = dt2 * S.V[i * NX + m] + dt * S.V[i * NX + 7 + m];
-        } else if (e < NX * NU + NU * NU) {
-          const int f = e - NX * NU, m = f / NU, n = f % NU;
-          const double wq = dt2 * S.V[m * NX + n] + dt * S.V[m * NX + 7 + n];
-          const double wv = dt2 * S.V[(7 + m) * NX + n] + dt * S.V[(7 + m) * NX + 7 + n];
-          S.Y[f] = dt2 * wq + dt * wv;
-        } else {
-          const int m = e - NX * NU - NU * NU;
-          S.z[m] = dt2 * S.Vx[m] + dt * S.Vx[7 + m];
         }
       }
+      if (l < NU * NU) {
+        const int m = l / NU, n = l - (l / NU) * NU;
+        const double wq = dt2 * S.V[m * NX + n] + dt * S.V[m * NX + 7 + n];
+        const double wv = dt2 * S.V[(7 + m) * NX + n] + dt * S.V[(7 + m) * NX + 7 + n];
+        S.Y[l] = dt2 * wq + dt * wv;
+      }
+      if (l < NU) S.z[l] = dt2 * S.Vx[l] + dt * S.Vx[7 + l];
       lds_sync();
-      // ---- phase B: M = I~'W + 1/2 A^'Y ; Qv = [Lx; Lu] + I~'Vx + A^'z ----
-      for (int e = l; e < ND * NU + ND; e += 64) {
-        int row[2];
-        double cf[2];
-        if (e < ND * NU) {
-          const int c = e / NU, m = e % NU;
-          const int nz = itilde<FF>(c, dt, alpha, beta, row, cf);
-          double acc = 0.0;
-          for (int q = 0; q < nz; ++q) acc += cf[q] * S.W[row[q] * NU + m];
+      // ---- phase B: row c = l of M = I~'W + 1/2 A^'Y ; Qv[c] = [Lx; Lu] + I~'Vx + A^'z ----
+      if (l < ND) {
+        const int c = l;
+        int r0, r1;
+        double a0, a1;
+        itilde2<FF>(c, dt, alpha, beta, r0, a0, r1, a1);
+        const double ac = (FF && c >= 21) ? 0.0 : 1.0;
+        const int cc = (FF && c >= 21) ? 0 : c;
+        double Acol[NU];
+#pragma unroll
+        for (int n = 0; n < NU; ++n) Acol[n] = ac * Ar[cc * 7 + n];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) {
           double h = 0.0;
 #pragma unroll
-          for (int n = 0; n < NU; ++n) h += ahat<FF>(Ar, n, c) * S.Y[n * NU + m];
-          S.M[e] = acc + 0.5 * h;
-        } else {
-          const int c = e - ND * NU;
-          const int nz = itilde<FF>(c, dt, alpha, beta, row, cf);
-          double acc = (c < NX) ? S.R[rec_off_Lx(NX) + c] : S.R[rec_off_Lu(NX) + c - NX];
-          for (int q = 0; q < nz; ++q) acc += cf[q] * S.Vx[row[q]];
-#pragma unroll
-          for (int m = 0; m < NU; ++m) acc += ahat<FF>(Ar, m, c) * S.z[m];
-          S.Qv[c] = acc;
+          for (int n = 0; n < NU; ++n) h += Acol[n] * S.Y[n * NU + m];
+          S.M[c * NU + m] = (a0 * S.W[r0 * NU + m] + a1 * S.W[r1 * NU + m]) + 0.5 * h;
         }
+        double qv = (c < NX) ? S.R[rec_off_Lx(NX) + c] : S.R[rec_off_Lu(NX) + c - NX];
+        qv += a0 * S.Vx[r0] + a1 * S.Vx[r1];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) qv += Acol[m] * S.z[m];
+        S.Qv[c] = qv;
       }
       lds_sync();
-      // ---- phase C: Q lower triangle (mirrored) ----
-      for (int e = l; e < ND * (ND + 1) / 2; e += 64) {
-        int r, c;
-        tri_rc(e, r, c);
-        double lv;
-        if (r < NX)
-          lv = S.R[rec_off_Lxx(NX) + r * NX + c];
-        else if (c < NX)
-          lv = S.R[rec_off_Lxu(NX) + c * NU + (r - NX)];
-        else
-          lv = S.R[rec_off_Luu(NX) + (r - NX) * NU + (c - NX)];
-        int rr[2], rc2[2];
-        double ar[2], ac[2];
-        const int nr = itilde<FF>(r, dt, alpha, beta, rr, ar);
-        const int nc2 = itilde<FF>(c, dt, alpha, beta, rc2, ac);
-        double g = 0.0;
-        for (int p = 0; p < nr; ++p)
-          for (int q = 0; q < nc2; ++q) g += ar[p] * ac[q] * S.V[rr[p] * NX + rc2[q]];
-        double h = 0.0;
+      // ---- phase C: Q lower triangle (mirrored), entries fixed per lane ----
+#pragma unroll 1
+      for (int k = 0; k < NQL; ++k) {
+        if (l + 64 * k < NQE) {
+          const int r = qrc[k] >> 8, c = qrc[k] & 255;
+          double lv;
+          if (r < NX)
+            lv = S.R[rec_off_Lxx(NX) + r * NX + c];
+          else if (c < NX)
+            lv = S.R[rec_off_Lxu(NX) + c * NU + (r - NX)];
+          else
+            lv = S.R[rec_off_Luu(NX) + (r - NX) * NU + (c - NX)];
+          int rr0, rr1, cr0, cr1;
+          double ra0, ra1, ca0, ca1;
+          itilde2<FF>(r, dt, alpha, beta, rr0, ra0, rr1, ra1);
+          itilde2<FF>(c, dt, alpha, beta, cr0, ca0, cr1, ca1);
+          const double g = ra0 * (ca0 * S.V[rr0 * NX + cr0] + ca1 * S.V[rr0 * NX + cr1]) +
+                           ra1 * (ca0 * S.V[rr1 * NX + cr0] + ca1 * S.V[rr1 * NX + cr1]);
+          const double sr = (FF && r >= 21) ? 0.0 : 1.0, sc = (FF && c >= 21) ? 0.0 : 1.0;
+          const int ir = (FF && r >= 21) ? 0 : r, ic = (FF && c >= 21) ? 0 : c;
+          double h1 = 0.0, h2 = 0.0;
 #pragma unroll
-        for (int m = 0; m < NU; ++m) h += S.M[r * NU + m] * ahat<FF>(Ar, m, c) + S.M[c * NU + m] * ahat<FF>(Ar, m, r);
-        double v = lv + g + h;
-        if (r == c && r >= NX) v += preg;
-        S.Q[r * ND + c] = v;
-        S.Q[c * ND + r] = v;
-        if (c >= NX) {
-          S.H[(r - NX) * NU + (c - NX)] = v;
-          S.H[(c - NX) * NU + (r - NX)] = v;
+          for (int m = 0; m < NU; ++m) {
+            h1 += S.M[r * NU + m] * Ar[ic * 7 + m];
+            h2 += S.M[c * NU + m] * Ar[ir * 7 + m];
+          }
+          double v = lv + g + (sc * h1 + sr * h2);
+          if (r == c && r >= NX) v += preg;
+          S.Q[r * ND + c] = v;
+          S.Q[c * ND + r] = v;
+          if (c >= NX) {
+            S.H[(r - NX) * NU + (c - NX)] = v;
+            S.H[(c - NX) * NU + (r - NX)] = v;
+          }
         }
       }
       lds_sync();
@@ -1278,9 +1314,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
       lds_sync();
       // ---- phase F: Vxx = sym(Qxx - Qxu K) + preg I (lower triangle, mirrored) ----
       int badv = 0;
-      for (int e = l; e < NX * (NX + 1) / 2; e += 64) {
-        int i, j;
-        tri_rc(e, i, j);
+#pragma unroll 1
+      for (int k = 0; k < NVL; ++k) {
+        if (l + 64 * k >= NVE) continue;
+        const int i = vij[k] >> 8, j = vij[k] & 255;
         double a1 = 0.0, a2 = 0.0;
 #pragma unroll
         for (int c = 0; c < NU; ++c) {
