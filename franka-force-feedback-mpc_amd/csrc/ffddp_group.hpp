@@ -16,25 +16,61 @@
 #pragma once
 
 #include "ffddp_node.hpp"
+#include "ffddp_prof.hpp"
 
 namespace ffddp {
 
 constexpr int G8 = 8;
 
 __device__ __forceinline__ int g8_lane() { return (int)(threadIdx.x & 7); }
-__device__ __forceinline__ double g8_get(double v, int src) { return __shfl(v, src, G8); }
-__device__ __forceinline__ double g8_up(double v, int d) { return __shfl_up(v, (unsigned)d, G8); }
-__device__ __forceinline__ double g8_down(double v, int d) { return __shfl_down(v, (unsigned)d, G8); }
+
+// Cross-lane moves inside the 8-lane group without going through LDS:
+// DPP row_shr / row_shl for the scans (groups are 8-aligned inside 16-lane
+// DPP rows; lanes whose source falls outside the group are masked by the
+// callers), ds_swizzle BROADCAST(8, k) for broadcasts, DPP half-mirror and
+// quad permutes for the sums.
+template <int CTRL> __device__ __forceinline__ double dpp64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL> __device__ __forceinline__ int dpp32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int K> __device__ __forceinline__ double g8_bc(double v) {
+  constexpr int off = 0x18 | (K << 5);  // swizzle bitmask mode: and 0x18, or K
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), off);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), off);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double g8_get(double v, int src) {
+  switch (src) {
+    case 0: return g8_bc<0>(v);
+    case 1: return g8_bc<1>(v);
+    case 2: return g8_bc<2>(v);
+    case 3: return g8_bc<3>(v);
+    case 4: return g8_bc<4>(v);
+    case 5: return g8_bc<5>(v);
+    case 6: return g8_bc<6>(v);
+    default: return g8_bc<7>(v);
+  }
+}
+__device__ __forceinline__ double g8_up(double v, int d) {
+  return d == 1 ? dpp64<0x111>(v) : (d == 2 ? dpp64<0x112>(v) : dpp64<0x114>(v));
+}
+__device__ __forceinline__ double g8_down(double v, int d) {
+  return d == 1 ? dpp64<0x101>(v) : (d == 2 ? dpp64<0x102>(v) : dpp64<0x104>(v));
+}
 __device__ __forceinline__ double g8_sum(double v) {
-  v += __shfl_xor(v, 4, G8);
-  v += __shfl_xor(v, 2, G8);
-  v += __shfl_xor(v, 1, G8);
+  v += dpp64<0x141>(v);  // row_half_mirror: lane i <-> 7 - i
+  v += dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
   return v;
 }
 __device__ __forceinline__ int g8_or(int v) {
-  v |= __shfl_xor(v, 4, G8);
-  v |= __shfl_xor(v, 2, G8);
-  v |= __shfl_xor(v, 1, G8);
+  v |= dpp32<0x141>(v);
+  v |= dpp32<0xB1>(v);
+  v |= dpp32<0x4E>(v);
   return v;
 }
 
@@ -45,7 +81,7 @@ __device__ __forceinline__ void g8_chol_rows(double (&a)[NQ], int li) {
     double d = a[k];
 #pragma unroll
     for (int m = 0; m < k; ++m) d -= a[m] * a[m];
-    const double il = 1.0 / sqrt(g8_get(d, k));
+    const double il = rsqrt_nr(g8_get(d, k));
     double s = a[k];
 #pragma unroll
     for (int m = 0; m < k; ++m) s -= a[m] * g8_get(a[m], k);
@@ -108,7 +144,11 @@ __device__ __forceinline__ void cross3(const double* a, const double* b, double*
 template <int NC>
 __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool surface, double q, double v, double u,
                                              double xq, double xv, double tr, const double* ref, double& qn,
-                                             double& vn, double& cpart, double (&lam)[3]) {
+                                             double& vn, double& cpart, double (&lam)[3]
+#ifdef FFDDP_PHASE_PROF
+                                             , unsigned long long (&pp_acc)[12], unsigned long long& pp_last
+#endif
+) {
   const ffddp_robot& rb = C.rb;
   const int li = g8_lane();
   const bool J = li < NQ;
@@ -162,6 +202,7 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
   double z[3] = {J ? R[2] : 0.0, J ? R[5] : 0.0, J ? R[8] : 0.0};
   double Sv[3];
   cross3(o, z, Sv);
+  PP(0);
   // ---- velocities: prefix sum of S qd ----
   const double Svq[3] = {Sv[0] * v, Sv[1] * v, Sv[2] * v};
   const double zq[3] = {z[0] * v, z[1] * v, z[2] * v};
@@ -211,6 +252,7 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
       }
     }
   }
+  PP(1);
   // ---- end-effector frame (lane 7 holds it after the scans) ----
   double pee[3], vp[3], wee[3], ap[3], Ree[9];
   {
@@ -233,6 +275,55 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
     for (int k = 0; k < 9; ++k) Ree[k] = g8_get(R[k], 7);
   }
 
+  PP(2);
+  // ---- costs that do not depend on the dynamics, computed by every lane with
+  // the same (broadcast) operands: no divergent EE-only block, so the
+  // scheduler can overlap them with the dynamics below ----
+  double cee;  // EE cost except the contact-force terms (uniform in the group)
+  {
+    double Rrel[9], rr[3], th;
+#pragma unroll
+    for (int a_ = 0; a_ < 3; ++a_)
+#pragma unroll
+      for (int b_ = 0; b_ < 3; ++b_)
+        Rrel[3 * a_ + b_] = C.Rdes[0 * 3 + a_] * Ree[0 * 3 + b_] + C.Rdes[1 * 3 + a_] * Ree[1 * 3 + b_] +
+                            C.Rdes[2 * 3 + a_] * Ree[2 * 3 + b_];
+    log3(Rrel, rr, th);
+    cee = C.w_ori * (0.5 * (C.ori_w[0] * rr[0] * rr[0] + C.ori_w[1] * rr[1] * rr[1] + C.ori_w[2] * rr[2] * rr[2]));
+    cee += C.w_wd * (0.5 * (C.wd_w[0] * wee[0] * wee[0] + C.wd_w[1] * wee[1] * wee[1] + C.wd_w[2] * wee[2] * wee[2]));
+    const double rx = pee[0] - ref[0], ry = pee[1] - ref[1], rz = pee[2] - ref[2];
+    const double cfree = C.w_ee_pos * (0.5 * (C.ee_pos_w[0] * rx * rx + C.ee_pos_w[1] * ry * ry + C.ee_pos_w[2] * rz * rz));
+    const double vx = vp[0] - ref[3], vy = vp[1] - ref[4];
+    double ccon = C.w_tp * (0.5 * (rx * rx + ry * ry)) + C.w_tv * (0.5 * (vx * vx + vy * vy));
+    if (C.has_pz) {
+      const double pz = pee[2] - (ref[2] - C.z_press);
+      ccon += C.w_pz * (0.5 * pz * pz);
+    }
+    if (C.has_vz) ccon += C.w_vz * (0.5 * vp[2] * vp[2]);
+    cee += surface ? ccon : cfree;
+  }
+  double cj = 0.0;  // this joint's state / control costs
+  if (J) {
+    if (C.variant == FFDDP_CLASSICAL || C.inner_state_reg) {
+      const double rq = q - xq, rv = v - xv;
+      cj += C.w_post * (0.5 * (rq * rq + rv * rv));
+      cj += C.w_v * (0.5 * (C.vdw[ji] * v * v));
+    }
+    if (C.has_qsoft) {
+      double ai, Ar, Arr;
+      barrier(q - C.qs_xref[ji], C.qs_lb[ji], C.qs_ub[ji], ai, Ar, Arr);
+      cj += C.w_qs * ai;
+    }
+    if (!terminal && (C.variant == FFDDP_CLASSICAL || C.inner_tau_reg)) {
+      const double r = u - tr;
+      cj += C.w_tau * (0.5 * r * r);
+      if (C.has_tsoft) {
+        double ai, Ar, Arr;
+        barrier(u, C.ts_lb[ji], C.ts_ub[ji], ai, Ar, Arr);
+        cj += C.w_ts * ai;
+      }
+    }
+  }
   lam[0] = lam[1] = lam[2] = 0.0;
   double a = 0.0;
   if (with_dyn) {
@@ -324,6 +415,7 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
       }
     }
     const double tau = Sv[0] * fl[0] + Sv[1] * fl[1] + Sv[2] * fl[2] + z[0] * fa[0] + z[1] * fa[1] + z[2] * fa[2];
+    PP(3);
     // CRBA column: F = Ic_j S_j ; M[k][j] = S_k . F  (k <= j), row j of the lower triangle on lane j
     double Fl[3], Fa[3];
     {
@@ -348,8 +440,10 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
 #pragma unroll
       for (int k = 0; k < NQ; ++k) Lr[k] = 0.0;
     }
+    PP(4);
     g8_chol_rows(Lr, li);
     double af = g8_solve(Lr, u - tau, li);
+    PP(5);
     if (surface) {
       constexpr int c0 = NC == 1 ? 2 : 0;
       const double pstar[3] = {ref[0], ref[1], ref[2] - C.z_press};
@@ -382,6 +476,7 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
       a = af;
     }
   }
+  PP(6);
   // ---- Euler step ----
   if (with_dyn) {
     const double dt = C.dt;
@@ -391,76 +486,32 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
     qn = q;
     vn = v;
   }
-  // ---- costs (this lane's share) ----
-  double c = 0.0;
-  if (J) {
-    if (C.variant == FFDDP_CLASSICAL || C.inner_state_reg) {
-      const double rq = q - xq, rv = v - xv;
-      c += C.w_post * (0.5 * (rq * rq + rv * rv));
-      c += C.w_v * (0.5 * (C.vdw[ji] * v * v));
-    }
-    if (C.has_qsoft) {
-      double ai, Ar, Arr;
-      barrier(q - C.qs_xref[ji], C.qs_lb[ji], C.qs_ub[ji], ai, Ar, Arr);
-      c += C.w_qs * ai;
-    }
-    if (!terminal && (C.variant == FFDDP_CLASSICAL || C.inner_tau_reg)) {
-      const double r = u - tr;
-      c += C.w_tau * (0.5 * r * r);
-      if (C.has_tsoft) {
+  // ---- contact-force costs (need lambda), then this lane's share ----
+  double cf = 0.0;
+  if (surface) {
+    double lm[3] = {0, 0, 0};
+    if (mode != MODE_TERMINAL_X)
+#pragma unroll
+      for (int r = 0; r < NC; ++r) lm[r] = lam[r];
+    if (C.has_uni) {
+#pragma unroll
+      for (int r = 0; r < NC; ++r) {
         double ai, Ar, Arr;
-        barrier(u, C.ts_lb[ji], C.ts_ub[ji], ai, Ar, Arr);
-        c += C.w_ts * ai;
+        barrier(lm[r], C.uni_lb[r], C.uni_ub[r], ai, Ar, Arr);
+        cf += C.w_uni * ai;
       }
     }
-  } else {
-    {  // ee_ori
-      double Rrel[9], rr[3], th;
+    if (C.has_fn) {
 #pragma unroll
-      for (int a_ = 0; a_ < 3; ++a_)
-#pragma unroll
-        for (int b_ = 0; b_ < 3; ++b_)
-          Rrel[3 * a_ + b_] = C.Rdes[0 * 3 + a_] * Ree[0 * 3 + b_] + C.Rdes[1 * 3 + a_] * Ree[1 * 3 + b_] +
-                              C.Rdes[2 * 3 + a_] * Ree[2 * 3 + b_];
-      log3(Rrel, rr, th);
-      c += C.w_ori * (0.5 * (C.ori_w[0] * rr[0] * rr[0] + C.ori_w[1] * rr[1] * rr[1] + C.ori_w[2] * rr[2] * rr[2]));
-    }
-    c += C.w_wd * (0.5 * (C.wd_w[0] * wee[0] * wee[0] + C.wd_w[1] * wee[1] * wee[1] + C.wd_w[2] * wee[2] * wee[2]));
-    if (!surface) {
-      const double rx = pee[0] - ref[0], ry = pee[1] - ref[1], rz = pee[2] - ref[2];
-      c += C.w_ee_pos * (0.5 * (C.ee_pos_w[0] * rx * rx + C.ee_pos_w[1] * ry * ry + C.ee_pos_w[2] * rz * rz));
-    } else {
-      const double rx = pee[0] - ref[0], ry = pee[1] - ref[1];
-      c += C.w_tp * (0.5 * (rx * rx + ry * ry));
-      const double vx = vp[0] - ref[3], vy = vp[1] - ref[4];
-      c += C.w_tv * (0.5 * (vx * vx + vy * vy));
-      if (C.has_pz) {
-        const double rz = pee[2] - (ref[2] - C.z_press);
-        c += C.w_pz * (0.5 * rz * rz);
-      }
-      if (C.has_vz) c += C.w_vz * (0.5 * vp[2] * vp[2]);
-      double lm[3] = {0, 0, 0};
-      if (mode != MODE_TERMINAL_X)
-#pragma unroll
-        for (int r = 0; r < NC; ++r) lm[r] = lam[r];
-      if (C.has_uni) {
-#pragma unroll
-        for (int r = 0; r < NC; ++r) {
-          double ai, Ar, Arr;
-          barrier(lm[r], C.uni_lb[r], C.uni_ub[r], ai, Ar, Arr);
-          c += C.w_uni * ai;
-        }
-      }
-      if (C.has_fn) {
-#pragma unroll
-        for (int r = 0; r < NC; ++r) {
-          const double e = lm[r] - C.fn_ref[r];
-          c += C.w_fn * (0.5 * C.fn_w[r] * e * e);
-        }
+      for (int r = 0; r < NC; ++r) {
+        const double e = lm[r] - C.fn_ref[r];
+        cf += C.w_fn * (0.5 * C.fn_w[r] * e * e);
       }
     }
   }
+  const double c = J ? cj : cee + cf;
   cpart = c;
+  PP(7);
 }
 
 }  // namespace ffddp

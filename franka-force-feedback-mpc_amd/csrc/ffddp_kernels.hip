@@ -53,6 +53,7 @@ struct InstState {
   double preg, cost, dg, dq, stop;
   int is_feasible, was_feasible, done, ok, iter, recalc, accepted, bw_ok;
   int n_iters, n_trials, n_retries, n_backward, n_calc, n_forward;
+  int fw_more;  // two-pass line search: first trials rejected, evaluate the rest
 };
 
 struct Dev {
@@ -105,6 +106,7 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
       s.accepted = -1;
       s.bw_ok = 0;
       s.n_iters = s.n_trials = s.n_retries = s.n_backward = s.n_calc = s.n_forward = 0;
+      s.fw_more = 0;
       d.st[i] = s;
     }
   }
@@ -938,7 +940,7 @@ __device__ __forceinline__ bool chol_rows(double (&a)[NU], int lane) {
     for (int m = 0; m < k; ++m) d -= a[m] * a[m];
     const double dk = bcast(d, k);
     if (!(dk > 0.0)) return false;
-    const double il = 1.0 / sqrt(dk);
+    const double il = rsqrt_nr(dk);
     double s = a[k];
 #pragma unroll
     for (int m = 0; m < k; ++m) s -= a[m] * bcast(a[m], k);
@@ -1069,6 +1071,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
   if (b >= d.B) return;
   InstState* st = d.st + b;
   if (st->done) return;
+#ifdef FFDDP_PHASE_PROF
+  const bool pp_on = (b == 0);
+#endif
+  PP_INIT();
   __shared__ S_t S;
   const bool feas = st->is_feasible != 0;
 #ifdef FFDDP_EXP_NOQP
@@ -1172,6 +1178,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
         }
       }
       lds_sync();
+      PP(0);
       const double* Ar = S.R + rec_off_A();
       // ---- phase A: W = V D (NX x 7), Y = D' V D (7 x 7), z = D' Vx ----
 #pragma unroll
@@ -1190,6 +1197,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
       }
       if (l < NU) S.z[l] = dt2 * S.Vx[l] + dt * S.Vx[7 + l];
       lds_sync();
+      PP(1);
       // ---- phase B: row c = l of M = I~'W + 1/2 A^'Y ; Qv[c] = [Lx; Lu] + I~'Vx + A^'z ----
       if (l < ND) {
         const int c = l;
@@ -1215,6 +1223,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
         S.Qv[c] = qv;
       }
       lds_sync();
+      PP(2);
       // ---- phase C: Q lower triangle (mirrored), entries fixed per lane ----
 #pragma unroll 1
       for (int k = 0; k < NQL; ++k) {
@@ -1252,6 +1261,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
         }
       }
       lds_sync();
+      PP(3);
       // ---- phase D: gains (Eigen::LLT or BoxQP), row / variable i on lane i ----
       {
         double hrow[NU], Lr[NU];
@@ -1288,6 +1298,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
             if (j <= l) S.L[tri(l, j)] = Lr[j];
       }
       lds_sync();
+      PP(4);
       // ---- phase E: K columns (and k for LLT) ----
       if (l < NX || (!use_qp && l == NX)) {
         double col[NU];
@@ -1312,6 +1323,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
         }
       }
       lds_sync();
+      PP(5);
       // ---- phase F: Vxx = sym(Qxx - Qxu K) + preg I (lower triangle, mirrored) ----
       int badv = 0;
 #pragma unroll 1
@@ -1330,6 +1342,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
         badv |= bad(fabs(v)) ? 1 : 0;
       }
       lds_sync();
+      PP(6);
       // ---- phase G: Vx, gap terms, expected improvement, k ----
       double cdg = 0.0, cdq = 0.0, cst = 0.0;
       if (l < NX) {
@@ -1370,6 +1383,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
       dq += cdq;
       stop += cst;
       lds_sync();
+      PP(7);
     }
     // ---- retry bookkeeping (SolverFDDP::solve: increaseRegularization) ----
     if (!failed) break;
@@ -1381,6 +1395,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
     }
     lds_sync();
   }
+  PP_FLUSH();
   if (l == 0) {
     st->preg = preg;
     st->n_retries += retries;
@@ -1487,7 +1502,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) 
                                                    const double* __restrict__ x0,
                                                    const double* __restrict__ node_ref,
                                                    const double* __restrict__ inst_ref,
-                                                   const uint8_t* __restrict__ surface) {
+                                                   const uint8_t* __restrict__ surface, int tr0, int ntr,
+                                                   int only_more) {
   const DevConsts& C = *Cg;
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
@@ -1495,10 +1511,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) 
   const int li = g8_lane();
   const bool J = li < NQ;
   const int ji = J ? li : 0;
-  const int b = (int)(gid / NTRIALS), tr = (int)(gid % NTRIALS);
+  const int b = (int)(gid / ntr), tr = tr0 + (int)(gid % ntr);
   if (b >= d.B) return;
   const InstState* st = d.st + b;
   if (st->done) return;
+  if (only_more && !st->fw_more) return;
+#ifdef FFDDP_PHASE_PROF
+  const bool pp_on = (b == 0 && tr == 0);
+#endif
+  PP_INIT();
   const double alpha = C.alphas[tr];
   const bool feas = st->is_feasible != 0;
   const bool gap = !(feas || alpha == 1.0);
@@ -1514,51 +1535,80 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) 
   bool fail = false;
   double* xtr = d.xs_try + ((long)b * NTRIALS + tr) * (N + 1) * nx;
   double* utr = d.us_try + ((long)b * NTRIALS + tr) * N * NU;
+  // node inputs of the rollout, prefetched one node ahead (joint lane ji)
+  constexpr int NCX = FF ? 3 : 2;  // state components per joint lane
+  double pxs[3] = {0, 0, 0}, pfs[3] = {0, 0, 0}, pw[3] = {0, 0, 0}, pK[21], pus = 0.0, pk = 0.0, pref[6];
+  auto fetch = [&](int t) {
+    const long nb = (long)b * (N + 1) + t;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) pref[c] = node_ref[nb * 6 + c];
+#pragma unroll
+    for (int c = 0; c < NCX; ++c) {
+      pxs[c] = J ? d.xs[nb * nx + 7 * c + ji] : 0.0;
+      pfs[c] = (J && gap) ? d.fs[nb * nx + 7 * c + ji] : 0.0;
+      pw[c] = (J && !feas) ? d.w[nb * nx + 7 * c + ji] : 0.0;
+    }
+    if (t < N) {
+      const long ub = (long)b * N + t;
+      pus = J ? d.us[ub * NU + ji] : 0.0;
+      pk = J ? d.k[ub * NU + ji] : 0.0;
+#ifdef FW_PREFETCH_K
+      const double* K_t = d.K + ub * NU * nx + (long)ji * nx;
+#pragma unroll
+      for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
+#endif
+    }
+  };
+  fetch(0);
   for (int t = 0; t <= N; ++t) {
-    const double* xs_t = d.xs + ((long)b * (N + 1) + t) * nx;
-    const double* fs_t = d.fs + ((long)b * (N + 1) + t) * nx;
     double xq_t = hq, xv_t = hv, xt_t = ht;
-    double sq = 0.0, sv = 0.0, stt = 0.0;
+    const double sq = pxs[0], sv = pxs[1], stt = pxs[2];
+    if (gap) {
+      xq_t = hq + pfs[0] * (alpha - 1.0);
+      xv_t = hv + pfs[1] * (alpha - 1.0);
+      if (FF) xt_t = ht + pfs[2] * (alpha - 1.0);
+    }
+    if (!feas) dvp -= pw[0] * (sq - xq_t) + pw[1] * (sv - xv_t) + (FF ? pw[2] * (stt - xt_t) : 0.0);
     if (J) {
-      sq = xs_t[ji];
-      sv = xs_t[7 + ji];
-      if (FF) stt = xs_t[14 + ji];
-      if (gap) {
-        xq_t = hq + fs_t[ji] * (alpha - 1.0);
-        xv_t = hv + fs_t[7 + ji] * (alpha - 1.0);
-        if (FF) xt_t = ht + fs_t[14 + ji] * (alpha - 1.0);
-      }
-      if (!feas) {
-        const double* w_t = d.w + ((long)b * (N + 1) + t) * nx;
-        dvp -= w_t[ji] * (sq - xq_t) + w_t[7 + ji] * (sv - xv_t) + (FF ? w_t[14 + ji] * (stt - xt_t) : 0.0);
-      }
       xtr[(long)t * nx + ji] = xq_t;
       xtr[(long)t * nx + 7 + ji] = xv_t;
       if (FF) xtr[(long)t * nx + 14 + ji] = xt_t;
     }
-    const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
+    double ref[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) ref[c] = pref[c];
     if (t < N) {
       // u_i = us_i - alpha k_i - K_i (x - xs)
       double u = 0.0;
       {
+#ifndef FW_PREFETCH_K
         const double* K_t = d.K + ((long)b * N + t) * NU * nx + (long)ji * nx;
-        double acc = J ? d.us[((long)b * N + t) * NU + ji] - d.k[((long)b * N + t) * NU + ji] * alpha : 0.0;
+#pragma unroll
+        for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
+#endif
+        double acc = pus - pk * alpha;
         const double dq = xq_t - sq, dv = xv_t - sv, dtt = xt_t - stt;
 #pragma unroll
         for (int m = 0; m < NQ; ++m) {
           const double dqm = g8_get(dq, m), dvm = g8_get(dv, m);
-          acc -= (J ? K_t[m] : 0.0) * dqm;
-          acc -= (J ? K_t[7 + m] : 0.0) * dvm;
-          if (FF) acc -= (J ? K_t[14 + m] : 0.0) * g8_get(dtt, m);
+          acc -= pK[m] * dqm;
+          acc -= pK[7 + m] * dvm;
+          if (FF) acc -= pK[14 + m] * g8_get(dtt, m);
         }
         // crocoddyl order: sum over x components 0..nx-1 (q then v then tau); rounding-level difference only
         if (C.use_box) acc = fmin(fmax(acc, C.u_lb[ji]), C.u_ub[ji]);
         u = acc;
         if (J) utr[(long)t * NU + ji] = u;
       }
+      fetch(t + 1);
       double qn, vn, cp, lam[3];
       const double uin = FF ? xt_t : u;
-      node_calc_g8<NC>(C, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam);
+      PP(8);
+      node_calc_g8<NC>(C, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam
+#ifdef FFDDP_PHASE_PROF
+                       , pp_acc, pp_last
+#endif
+      );
       double c = C.dt * cp;
       double tn = 0.0;
       if (FF) {
@@ -1584,7 +1634,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) 
     } else {
       double qn, vn, cp, lam[3];
       const int mode = FF ? MODE_TERMINAL_U : MODE_TERMINAL_X;
-      node_calc_g8<NC>(C, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam);
+      PP(8);
+      node_calc_g8<NC>(C, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam
+#ifdef FFDDP_PHASE_PROF
+                       , pp_acc, pp_last
+#endif
+      );
       double c = FF ? C.dt * cp : cp;
       if (FF && J) {
         const double e1 = xq_t - yref[ji], e2 = xv_t - yref[7 + ji], e3 = xt_t - yref[14 + ji];
@@ -1594,6 +1649,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) 
       if (bad(cost)) fail = true;
     }
   }
+  PP(9);
+  PP_FLUSH_AT(16);
   const double dv = g8_sum(dvp);
   if (li == 0) {
     d.trial[((long)b * NTRIALS + tr) * 2 + 0] = cost;
@@ -1605,6 +1662,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) 
 // ---------------------------------------------------------------------------
 // acceptance / regularisation / stopping: one lane per instance
 // ---------------------------------------------------------------------------
+// SolverFDDP::tryStep acceptance of trial tr for an instance in state s
+__device__ __forceinline__ bool trial_accepted(const DevConsts& C, const Dev& d, const InstState& s, int b, int tr) {
+  if (d.trial_fail[(long)b * NTRIALS + tr]) return false;
+  const double a = C.alphas[tr];
+  const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
+  const double dv = s.is_feasible ? 0.0 : d.trial[((long)b * NTRIALS + tr) * 2 + 1];
+  const double dV = s.cost - cost_try;
+  const double d0 = s.dg + dv, d1 = s.dq - 2.0 * dv;
+  const double dVexp = a * (d0 + 0.5 * a * d1);
+  if (dVexp >= 0) return fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp;
+  return fabs(d0) < C.th_grad || dV > C.th_acceptnegstep * dVexp;  // gap-closing branch
+}
+
+// two-pass line search: does any of the first ntr trials pass?
+__global__ void k_probe(const DevConsts* __restrict__ Cg, Dev d, int ntr) {
+  const DevConsts& C = *Cg;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= d.B) return;
+  InstState& s = d.st[b];
+  if (s.done) return;
+  bool any = false;
+  for (int tr = 0; tr < ntr && !any; ++tr) any = trial_accepted(C, d, s, b, tr);
+  s.fw_more = any ? 0 : 1;
+}
+
 __global__ void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter) {
   const DevConsts& C = *Cg;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1619,19 +1701,9 @@ __global__ void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter) {
   double steplength = C.alphas[NTRIALS - 1];
   int tried = NTRIALS;
   for (int tr = 0; tr < NTRIALS; ++tr) {
-    if (d.trial_fail[(long)b * NTRIALS + tr]) continue;
     const double a = C.alphas[tr];
     const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
-    const double dv = s.is_feasible ? 0.0 : d.trial[((long)b * NTRIALS + tr) * 2 + 1];
-    const double dV = s.cost - cost_try;
-    const double d0 = s.dg + dv, d1 = s.dq - 2.0 * dv;
-    const double dVexp = a * (d0 + 0.5 * a * d1);
-    bool ok;
-    if (dVexp >= 0)
-      ok = fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp;
-    else  // gap-closing branch: cost may rise by up to th_acceptnegstep x the prediction
-      ok = fabs(d0) < C.th_grad || dV > C.th_acceptnegstep * dVexp;
-    if (ok) {
+    if (trial_accepted(C, d, s, b, tr)) {
       acc = tr;
       steplength = a;
       tried = tr + 1;
@@ -1746,8 +1818,16 @@ struct ffddp_handle {
   int32_t *out_iters = nullptr, *out_stats = nullptr;
   uint8_t* out_ok = nullptr;
   std::string err;
+  // sub-batch streams: the batch is split into nstreams slices solved on their
+  // own HIP streams, so latency-bound phases of one slice overlap with the
+  // throughput-bound phases of another (FFDDP_STREAMS, default 3: with the
+  // caller's stream that is the 4 hardware queues a process gets)
+  int nstreams = 3;
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> sev;  // fork + per-stream join events
   bool bw_wave = true;
-  bool fw_group = false;  // 8-lane joint-parallel line search (FFDDP_FW=group); default one lane per trial  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
+  int fw_first = 3;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
+  bool fw_group = true;  // 8-lane joint-parallel line search; FFDDP_FW=lane selects one lane per trial  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
   // optional per-kernel timing
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -1933,64 +2013,149 @@ struct ProfScope {
 
 enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE };
 
+// the per-instance slice [b0, b0 + Bk) of the handle workspace
+Dev dev_slice(const Dev& d0, int b0, int Bk) {
+  Dev d = d0;
+  const long N = d0.N, nx = d0.nx;
+  d.B = Bk;
+  d.rec_buf += (long)b0 * (N + 1) * d0.rec;
+  d.fs += (long)b0 * (N + 1) * nx;
+  d.xs += (long)b0 * (N + 1) * nx;
+  d.us += (long)b0 * N * NU;
+  d.K += (long)b0 * N * NU * nx;
+  d.k += (long)b0 * N * NU;
+  d.w += (long)b0 * (N + 1) * nx;
+  d.xs_try += (long)b0 * NTRIALS * (N + 1) * nx;
+  d.us_try += (long)b0 * NTRIALS * N * NU;
+  d.trial += (long)b0 * NTRIALS * 2;
+  d.trial_fail += (long)b0 * NTRIALS;
+  d.st += b0;
+  d.prim += (long)b0 * (N + 1);
+  d.link += (long)b0 * (N + 1) * LK_ALLOC;
+  return d;
+}
+
 template <int NC, bool FF>
 int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref, const double* iref,
                  const uint8_t* surf, const double* xs_init, const double* us_init, int maxiter, int is_feasible,
                  double* xs, double* us, double* K, double* cost, int32_t* iters, uint8_t* ok, double* fn_pred,
                  int32_t* stats, hipStream_t s) {
-  Dev d = h->d;
-  d.B = B;
   const int N = h->hc.N, nx = h->hc.nx;
-  {
-    ProfScope p(h, s, KC_INIT);
-    hipLaunchKernelGGL(k_init, dim3(1024), dim3(256), 0, s, h->dc, d, xs_init, us_init, is_feasible);
+  int S = h->nstreams;
+  if (B < 64 * S) S = 1;
+  if (S > 1 && (int)h->streams.size() < S) {
+    while ((int)h->streams.size() < S) {
+      hipStream_t st;
+      HIPCHK(h, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      h->streams.push_back(st);
+    }
+    while ((int)h->sev.size() < S + 1) {
+      hipEvent_t e;
+      HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      h->sev.push_back(e);
+    }
   }
-  const long nodes = (long)B * (N + 1);
-  const int node_blocks = (int)((nodes + NODE_GPB - 1) / NODE_GPB);
-  const int fw_blocks = (int)(((long)B * NTRIALS + FW_BLOCK - 1) / FW_BLOCK);
+  const int Bs = (B + S - 1) / S;
+  struct Slice {
+    Dev d;
+    hipStream_t s;
+    int b0, B;
+  };
+  Slice sl[8];
+  for (int k = 0; k < S; ++k) {
+    sl[k].b0 = k * Bs;
+    sl[k].B = (B - sl[k].b0) < Bs ? (B - sl[k].b0) : Bs;
+    sl[k].d = dev_slice(h->d, sl[k].b0, sl[k].B);
+    sl[k].s = S > 1 ? h->streams[k] : s;
+  }
+  if (S > 1) {
+    HIPCHK(h, hipEventRecord(h->sev[0], s));
+    for (int k = 0; k < S; ++k) HIPCHK(h, hipStreamWaitEvent(sl[k].s, h->sev[0], 0));
+  }
+  const long nxl = nx, N1 = N + 1;
+  for (int k = 0; k < S; ++k) {
+    ProfScope p(h, sl[k].s, KC_INIT);
+    const long b0 = sl[k].b0;
+    hipLaunchKernelGGL(k_init, dim3(1024), dim3(256), 0, sl[k].s, h->dc, sl[k].d, xs_init + b0 * N1 * nxl,
+                       us_init + b0 * (long)N * NU, is_feasible);
+  }
   for (int it = 0; it < maxiter; ++it) {
-    {
-      ProfScope p(h, s, KC_NODE);
-      hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, s, h->dc, d, x0, nref, iref,
-                         surf, 0);
-      hipLaunchKernelGGL((k_node<NC, FF>), dim3(node_blocks), dim3(NODE_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf, 0);
-    }
-    {
-      ProfScope p(h, s, KC_BACKWARD);
-      if (h->bw_wave)
-        hipLaunchKernelGGL((k_backward_w<FF>), dim3(B), dim3(64), 0, s, h->dc, d, it);
-      else
-        hipLaunchKernelGGL((k_backward<FF>), dim3((B + (FF ? 1 : 3)) / (FF ? 2 : 4)), dim3(BW_BLOCK), 0, s, h->dc, d, it);
-    }
-    {
-      ProfScope p(h, s, KC_FORWARD);
-      if (h->fw_group)
-        hipLaunchKernelGGL((k_forward_g8<NC, FF>), dim3((int)(((long)B * NTRIALS * G8 + 63) / 64)), dim3(64), 0, s, h->dc,
-                           d, x0, nref, iref, surf);
-      else
-        hipLaunchKernelGGL((k_forward<NC, FF>), dim3(fw_blocks), dim3(FW_BLOCK), 0, s, h->dc, d, x0, nref, iref, surf);
-    }
-    {
-      ProfScope p(h, s, KC_ACCEPT);
-      hipLaunchKernelGGL(k_accept, dim3((B + 255) / 256), dim3(256), 0, s, h->dc, d, it);
-    }
-    {
-      ProfScope p(h, s, KC_COMMIT);
-      hipLaunchKernelGGL(k_commit, dim3(2048), dim3(256), 0, s, h->dc, d);
+    for (int k = 0; k < S; ++k) {
+      const Dev& d = sl[k].d;
+      const hipStream_t ss = sl[k].s;
+      const int Bk = sl[k].B;
+      const long b0 = sl[k].b0;
+      const double* x0k = x0 + b0 * nxl;
+      const double* nrefk = nref + b0 * N1 * 6;
+      const double* irefk = iref + b0 * 21;
+      const uint8_t* surfk = surf + b0;
+      const long nodes = (long)Bk * (N + 1);
+      {
+        ProfScope p(h, ss, KC_NODE);
+        hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k, nrefk,
+                           irefk, surfk, 0);
+        hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, ss,
+                           h->dc, d, x0k, nrefk, irefk, surfk, 0);
+      }
+      {
+        ProfScope p(h, ss, KC_BACKWARD);
+        if (h->bw_wave)
+          hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it);
+        else
+          hipLaunchKernelGGL((k_backward<FF>), dim3((Bk + (FF ? 1 : 3)) / (FF ? 2 : 4)), dim3(BW_BLOCK), 0, ss, h->dc, d,
+                             it);
+      }
+      {
+        ProfScope p(h, ss, KC_FORWARD);
+        if (h->fw_group) {
+          const int n1 = h->fw_first;
+          hipLaunchKernelGGL((k_forward_g8<NC, FF>), dim3((int)(((long)Bk * n1 * G8 + 63) / 64)), dim3(64), 0, ss, h->dc,
+                             d, x0k, nrefk, irefk, surfk, 0, n1, 0);
+          if (n1 < NTRIALS) {
+            hipLaunchKernelGGL(k_probe, dim3((Bk + 255) / 256), dim3(256), 0, ss, h->dc, d, n1);
+            hipLaunchKernelGGL((k_forward_g8<NC, FF>), dim3((int)(((long)Bk * (NTRIALS - n1) * G8 + 63) / 64)),
+                               dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk, n1, NTRIALS - n1, 1);
+          }
+        } else {
+          hipLaunchKernelGGL((k_forward<NC, FF>), dim3((int)(((long)Bk * NTRIALS + FW_BLOCK - 1) / FW_BLOCK)),
+                             dim3(FW_BLOCK), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk);
+        }
+      }
+      {
+        ProfScope p(h, ss, KC_ACCEPT);
+        hipLaunchKernelGGL(k_accept, dim3((Bk + 255) / 256), dim3(256), 0, ss, h->dc, d, it);
+      }
+      {
+        ProfScope p(h, ss, KC_COMMIT);
+        hipLaunchKernelGGL(k_commit, dim3(2048), dim3(256), 0, ss, h->dc, d);
+      }
     }
   }
-  {
-    ProfScope p(h, s, KC_FINALIZE);
-    hipLaunchKernelGGL((k_finalize<NC, FF>), dim3((2 * B + 63) / 64), dim3(64), 0, s, h->dc, d, maxiter, x0, nref,
-                       iref, surf, cost, iters, ok, fn_pred, stats);
+  const size_t bxs = (size_t)(N + 1) * nx * sizeof(double);
+  const size_t bus = (size_t)N * NU * sizeof(double);
+  const size_t bks = (size_t)N * NU * nx * sizeof(double);
+  for (int k = 0; k < S; ++k) {
+    const Dev& d = sl[k].d;
+    const hipStream_t ss = sl[k].s;
+    const long b0 = sl[k].b0;
+    const int Bk = sl[k].B;
+    {
+      ProfScope p(h, ss, KC_FINALIZE);
+      hipLaunchKernelGGL((k_finalize<NC, FF>), dim3((2 * Bk + 63) / 64), dim3(64), 0, ss, h->dc, d, maxiter,
+                         x0 + b0 * nxl, nref + b0 * N1 * 6, iref + b0 * 21, surf + b0, cost + b0, iters + b0, ok + b0,
+                         fn_pred ? fn_pred + 2 * b0 : nullptr, stats ? stats + b0 * FFDDP_NSTATS : nullptr);
+    }
+    HIPCHK(h, hipMemcpyAsync(xs + b0 * N1 * nxl, d.xs, bxs * Bk, hipMemcpyDeviceToDevice, ss));
+    HIPCHK(h, hipMemcpyAsync(us + b0 * (long)N * NU, d.us, bus * Bk, hipMemcpyDeviceToDevice, ss));
+    HIPCHK(h, hipMemcpyAsync(K + b0 * (long)N * NU * nx, d.K, bks * Bk, hipMemcpyDeviceToDevice, ss));
   }
   if (hipGetLastError() != hipSuccess) return fail(h, FFDDP_E_DEVICE, "kernel launch failed");
-  const size_t bx = (size_t)B * (N + 1) * nx * sizeof(double);
-  const size_t bu = (size_t)B * N * NU * sizeof(double);
-  const size_t bk = (size_t)B * N * NU * nx * sizeof(double);
-  HIPCHK(h, hipMemcpyAsync(xs, d.xs, bx, hipMemcpyDeviceToDevice, s));
-  HIPCHK(h, hipMemcpyAsync(us, d.us, bu, hipMemcpyDeviceToDevice, s));
-  HIPCHK(h, hipMemcpyAsync(K, d.K, bk, hipMemcpyDeviceToDevice, s));
+  if (S > 1) {
+    for (int k = 0; k < S; ++k) {
+      HIPCHK(h, hipEventRecord(h->sev[1 + k], sl[k].s));
+      HIPCHK(h, hipStreamWaitEvent(s, h->sev[1 + k], 0));
+    }
+  }
   return 0;
 }
 
@@ -2051,8 +2216,18 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   {
     const char* bw = std::getenv("FFDDP_BW");
     h->bw_wave = !(bw && std::strcmp(bw, "group") == 0);
+    const char* ns = std::getenv("FFDDP_STREAMS");
+    if (ns) {
+      const int v = std::atoi(ns);
+      h->nstreams = v < 1 ? 1 : (v > 8 ? 8 : v);
+    }
     const char* fw = std::getenv("FFDDP_FW");
-    h->fw_group = fw && std::strcmp(fw, "group") == 0;
+    h->fw_group = !(fw && std::strcmp(fw, "lane") == 0);
+    const char* f1 = std::getenv("FFDDP_FW_FIRST");
+    if (f1) {
+      const int v = std::atoi(f1);
+      h->fw_first = v < 1 ? 1 : (v > NTRIALS ? NTRIALS : v);
+    }
   }
   int rc = 0;
   rc |= dalloc(h, &h->dc, 1);
@@ -2100,6 +2275,17 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   return 0;
 }
 
+#ifdef FFDDP_PHASE_PROF
+extern "C" int ffddp_debug_phase_read(unsigned long long* out, int n, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ffddp::g_pp), sizeof(unsigned long long) * (n < 32 ? n : 32)) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ffddp::g_pp), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
+
 int ffddp_profile_enable(ffddp_handle* h, int on) {
   if (!h) return FFDDP_E_INVALID;
   h->prof = on != 0;
@@ -2134,6 +2320,8 @@ void ffddp_destroy(ffddp_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->sev) (void)hipEventDestroy(e);
+  for (hipStream_t st : h->streams) (void)hipStreamDestroy(st);
   free_all(h);
   delete h;
 }

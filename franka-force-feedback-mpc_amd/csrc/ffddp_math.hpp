@@ -116,6 +116,22 @@ template <class T> FFD_HD V3<T> cmul(const double* I, V3<T> x) {
 // ---------------------------------------------------------------------------
 FFD_HD int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
+// 1/sqrt(d) for d > 0: hardware estimate refined by two Newton steps (full
+// double precision, within an ulp or so of the correctly rounded quotient)
+// instead of a correctly rounded sqrt followed by a division; both are long
+// dependent sequences on CDNA and sit on the critical path of every LLT.
+FFD_HD double rsqrt_nr(double d) {
+#ifdef __HIP_DEVICE_COMPILE__
+  double y = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d;
+  y = y * (1.5 - h * y * y);
+  y = y * (1.5 - h * y * y);
+  return y;
+#else
+  return 1.0 / sqrt(d);
+#endif
+}
+
 template <int N> FFD_HD bool chol_packed(double* A /* packed lower, in-place */) {
 #pragma unroll
   for (int j = 0; j < N; ++j) {
@@ -123,7 +139,7 @@ template <int N> FFD_HD bool chol_packed(double* A /* packed lower, in-place */)
 #pragma unroll
     for (int k = 0; k < j; ++k) d -= A[tri(j, k)] * A[tri(j, k)];
     if (!(d > 0.0)) return false;
-    const double il = 1.0 / sqrt(d);
+    const double il = rsqrt_nr(d);
     A[tri(j, j)] = il;
 #pragma unroll
     for (int i = j + 1; i < N; ++i) {
