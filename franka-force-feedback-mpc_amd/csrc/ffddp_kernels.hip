@@ -1826,7 +1826,7 @@ struct ffddp_handle {
   std::vector<hipStream_t> streams;
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
   bool bw_wave = true;
-  int fw_first = 3;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
+  int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
   bool fw_group = true;  // 8-lane joint-parallel line search; FFDDP_FW=lane selects one lane per trial  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
   // optional per-kernel timing
   bool prof = false;

@@ -11,11 +11,11 @@ for flags in "$@"; do
     tail -1 gpurun_out/ab_tests.log
   fi
   first=0
-  timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-io $BENCH_ARGS > gpurun_out/ab_bench.log 2>&1 || { tail -20 gpurun_out/ab_bench.log; exit 1; }
+  timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-io $BENCH_ARGS $AB_ARGS > gpurun_out/ab_bench.log 2>&1 || { tail -20 gpurun_out/ab_bench.log; exit 1; }
   python - "$flags" <<'PY'
 import json,sys
 l=[x for x in open("gpurun_out/ab_bench.log") if x.startswith("{")][-1]
 j=json.loads(l)
-print(repr(sys.argv[1]), "value %.0f" % j["value"], "ms %.2f" % j["ms_per_step"], " ".join("%s=%.2f" % (k, v["ms_per_step"]) for k, v in j["kernels"].items() if v["ms_per_step"] > 0.2), "ok=%.3f it=%.2f" % (j["solver"]["ok_frac"], j["solver"]["mean_iter"]))
+print(repr(sys.argv[1]), "value %.0f" % j["value"], "ms %.2f" % j["ms_per_step"], " ".join("%s=%.2f" % (k, v["ms_per_step"]) for k, v in (j["kernels"] or {}).items() if v["ms_per_step"] > 0.2), "ok=%.3f it=%.2f" % (j["solver"]["ok_frac"], j["solver"]["mean_iter"]))
 PY
 done
