@@ -1830,6 +1830,7 @@ struct ffddp_handle {
   bool fw_group = true;  // 8-lane joint-parallel line search; FFDDP_FW=lane selects one lane per trial  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
   // optional per-kernel timing
   bool prof = false;
+  int prof_mask = 0;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<int> ev_class;  // class per event pair
@@ -1992,8 +1993,9 @@ void free_all(ffddp_handle* h) {
 struct ProfScope {
   ffddp_handle* h;
   hipStream_t s;
-  ProfScope(ffddp_handle* h_, hipStream_t s_, int cls) : h(h_), s(s_) {
-    if (!h->prof) return;
+  bool on;
+  ProfScope(ffddp_handle* h_, hipStream_t s_, int cls) : h(h_), s(s_), on(h_->prof && ((h_->prof_mask >> cls) & 1)) {
+    if (!on) return;
     if (h->ev_used + 2 > h->ev_pool.size()) {
       for (int i = 0; i < 256; ++i) {
         hipEvent_t e;
@@ -2005,7 +2007,7 @@ struct ProfScope {
     (void)hipEventRecord(h->ev_pool[h->ev_used], s);
   }
   ~ProfScope() {
-    if (!h->prof) return;
+    if (!on) return;
     (void)hipEventRecord(h->ev_pool[h->ev_used + 1], s);
     h->ev_used += 2;
   }
@@ -2286,9 +2288,10 @@ extern "C" int ffddp_debug_phase_read(unsigned long long* out, int n, int reset)
 }
 #endif
 
-int ffddp_profile_enable(ffddp_handle* h, int on) {
+int ffddp_profile_enable(ffddp_handle* h, int classes) {
   if (!h) return FFDDP_E_INVALID;
-  h->prof = on != 0;
+  h->prof_mask = classes & FFDDP_PROFILE_ALL;
+  h->prof = h->prof_mask != 0;
   return 0;
 }
 

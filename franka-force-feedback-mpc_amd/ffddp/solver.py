@@ -105,8 +105,18 @@ class BatchedBoxFDDP:
         self._check(rc, "ffddp_solve_batch_dev")
 
     # -- per-kernel device timing ----------------------------------------------------
-    def profile(self, on: bool = True):
-        self._check(self._lib.ffddp_profile_enable(self._h, int(on)), "ffddp_profile_enable")
+    def profile(self, on=True):
+        """on: True (every kernel class), False, or an iterable of class names
+        from _abi.KERNEL_CLASSES to time only those."""
+        if on is True:
+            mask = (1 << len(_abi.KERNEL_CLASSES)) - 1
+        elif not on:
+            mask = 0
+        else:
+            mask = 0
+            for name in on:
+                mask |= 1 << _abi.KERNEL_CLASSES.index(name)
+        self._check(self._lib.ffddp_profile_enable(self._h, int(mask)), "ffddp_profile_enable")
 
     def profile_read(self, reset: bool = True) -> dict:
         ms = np.zeros(len(_abi.KERNEL_CLASSES))

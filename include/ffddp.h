@@ -153,9 +153,13 @@ int ffddp_gravity_torque(const ffddp_robot* robot, int B, const double* q, doubl
 /* Optional per-kernel device timing (HIP events recorded around every launch
  * on the launch stream).  Kernel classes, in order: init, node (calc+calcDiff),
  * backward, forward (line search), accept, commit, finalize.
+ * `classes` is a bit mask over those classes (bit i = class i; 0 = off,
+ * FFDDP_PROFILE_ALL = every class).  Timing only the kernel of interest keeps
+ * the event overhead out of the other launches.
  * ffddp_profile_read synchronises the recorded events and returns, per class,
  * the summed milliseconds and launch counts since the last reset. */
-int ffddp_profile_enable(ffddp_handle* h, int on);
+#define FFDDP_PROFILE_ALL 0x7F
+int ffddp_profile_enable(ffddp_handle* h, int classes);
 int ffddp_profile_read(ffddp_handle* h, double* ms, int64_t* launches, int reset);
 
 /* Batched gravity torque on the device (tau_ref for B instances), device pointers. */

@@ -12,7 +12,7 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o 
 echo "fetch done"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o r01 -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile > $O/write_bench.log 2>&1
 echo "write done"
-python3 $R/tools/pmc_traffic.py $O/fetch $O/write classical/normal_1d/B4096/N30 $O/traffic_latest.json
+python3 $R/tools/pmc_traffic.py $O/fetch $O/write classical/normal_1d/B4096/N30 3 $O/traffic_latest.json
 cp $O/traffic_latest.json $R/profiles/traffic_latest.json
 timeout -k 10 400 python3 $R/bench.py > $O/bench_full.log 2>&1
 echo "bench done"

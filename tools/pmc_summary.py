@@ -4,14 +4,12 @@ import csv, sys
 from collections import defaultdict
 from pathlib import Path
 
-CLASSES = ("node", "backward_w", "backward", "forward", "primal", "accept", "commit", "init", "finalize")
+import re
 
 
 def kclass(n):
-    for c in CLASSES:
-        if f"k_{c}<" in n or f"k_{c}(" in n:
-            return c
-    return None
+    m = re.search(r"k_[a-z0-9_]+", n)
+    return m.group(0)[2:] if m else None
 
 
 tot = defaultdict(lambda: defaultdict(float))
@@ -21,6 +19,10 @@ for f in Path(sys.argv[1]).rglob("*counter_collection.csv"):
         c = kclass(low.get("kernel_name", ""))
         if c:
             tot[c][low["counter_name"]] += float(low["counter_value"])
+busy = 0.0
+for c, d in tot.items():
+    busy += d.get("SQ_ACTIVE_INST_VALU", 0.0) * 4
+print(f"VALU-active cycles (all kernels): {busy:.4g}  = {busy / 1024 / 2.4e9 * 1e3:.3f} ms of all 1024 SIMDs at 2.4 GHz")
 for c, d in tot.items():
     w = d.get("SQ_WAVES", 0) or 1
     print(f"== {c}: waves {w:.0f}")

@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-launch HBM
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-solve HBM
 bytes for the solver kernels (MI355X_MICROARCH.md §HBM: FETCH_SIZE is reported
 in KiB and counts half the bytes of wide streaming reads on gfx950, so it is
 doubled; WRITE_SIZE is taken as is).
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON
-  CONFIG is bench.py's "<variant>/<contact>/B<B>/N<N>" key.
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG SOLVES OUT_JSON
+  CONFIG is bench.py's "<variant>/<contact>/B<B>/N<N>" key; SOLVES the number
+  of batched solves each profiled run executed (warmup + steps).  Bytes are
+  reported per solve per kernel class (bench.py divides by its own launch
+  count of that class).
 """
 from __future__ import annotations
 
@@ -15,12 +18,17 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-CLASSES = ("node", "backward", "forward", "primal", "accept", "commit", "init", "finalize")
+# kernel name -> bench/profiler class (ffddp_profile_read classes)
+CLASS_OF = (
+    ("k_primal", "node"), ("k_node", "node"), ("k_backward", "backward"), ("k_forward", "forward"),
+    ("k_probe", "forward"), ("k_accept", "accept"), ("k_commit", "commit"), ("k_init", "init"),
+    ("k_finalize", "finalize"),
+)
 
 
 def kclass(name: str):
-    for c in CLASSES:
-        if f"k_{c}" in name:
+    for key, c in CLASS_OF:
+        if key in name:
             return c
     return None
 
@@ -47,21 +55,22 @@ def read_counter(d: Path, counter: str):
 
 
 def main():
-    fetch_dir, write_dir, config, out = sys.argv[1:5]
+    fetch_dir, write_dir, config, solves, out = sys.argv[1:6]
+    solves = float(solves)
     fe = read_counter(Path(fetch_dir), "FETCH_SIZE")
     wr = read_counter(Path(write_dir), "WRITE_SIZE")
     kernels = {}
     for c in sorted(set(fe) & set(wr)):
         f_kib, nf = fe[c]
         w_kib, nw = wr[c]
-        fetch_b = 2.0 * f_kib * 1024.0 / max(1, nf)
-        write_b = w_kib * 1024.0 / max(1, nw)
+        fetch_b = 2.0 * f_kib * 1024.0 / solves
+        write_b = w_kib * 1024.0 / solves
         kernels[c] = {
-            "hbm_bytes_per_launch": fetch_b + write_b,
-            "fetch_bytes_per_launch": fetch_b,
-            "write_bytes_per_launch": write_b,
-            "launches_fetch_pass": nf,
-            "launches_write_pass": nw,
+            "hbm_bytes_per_solve": fetch_b + write_b,
+            "fetch_bytes_per_solve": fetch_b,
+            "write_bytes_per_solve": write_b,
+            "dispatches_fetch_pass": nf,
+            "dispatches_write_pass": nw,
         }
     res = {
         "config": config,
