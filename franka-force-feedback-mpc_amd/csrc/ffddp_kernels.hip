@@ -45,6 +45,9 @@ constexpr int FW_BLOCK = 64;
 #ifndef FW_WAVES
 #define FW_WAVES 2
 #endif
+#ifndef QC_UNROLL
+#define QC_UNROLL 1
+#endif
 #ifndef BW_WAVES
 #define BW_WAVES 1
 #endif
@@ -855,7 +858,7 @@ template <bool FF> struct BwW {
   static constexpr int NX = FF ? 21 : 14;
   static constexpr int ND = NX + NU;
   static constexpr int REC = rec_words(NX);
-  double R[REC];      // staged node record (A | Lxx | Lxu | Luu | Lx | Lu | cost | lam)
+  double R[(REC + 63) / 64 * 64];  // staged node record (A | Lxx | Lxu | Luu | Lx | Lu | cost | lam), padded
   double V[NX * NX];  // V_xx' on entry to a node, V_xx on exit
   double Q[ND * ND];  // [[Qxx, Qxu], [Qux, Quu + preg I]]
   double W[NX * NU];  // V D
@@ -864,7 +867,8 @@ template <bool FF> struct BwW {
   double K[NU * NX];
   double H[NU * NU];  // Quu + preg I (contiguous copy for the gains lane)
   double L[28];       // packed (masked) Cholesky factor, reciprocal diagonal
-  double Vx[NX], Qv[ND], fs[NX], kk[NU], z[NU], kp[NU], uu[NU];
+  double Vx[NX], Qv[ND], kk[NU], z[NU];
+  double fs[64], kp[64], uu[64], ulb[64], uub[64];  // one slot per lane: written without lane guards
   int flag;
   int clamped[NU];
 };
@@ -1013,14 +1017,12 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
     }
     const double dx = cl ? 0.0 : xsf - x;
     double dmax = 0.0;
-    double dxb[NU], gb[NU];
 #pragma unroll
-    for (int j = 0; j < NU; ++j) {
-      dxb[j] = bcast(dx, j);
-      gb[j] = bcast(g, j);
-      dmax = fmax(dmax, fabs(dxb[j]));
-    }
+    for (int j = 0; j < NU; ++j) dmax = fmax(dmax, fabs(bcast(dx, j)));
     if (dmax < C.qp_th_grad) break;
+    double gb[NU];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) gb[j] = bcast(g, j);
     double fold;
     {
       double hx = 0.0;
@@ -1097,6 +1099,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
   int retries = 0;
   bool fail_inst = false;
   double dg = 0.0, dq = 0.0, stop = 0.0;
+  S.ulb[l] = C.u_lb[l < NU ? l : NU - 1];
+  S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
   // this lane's lower-triangle entries of Q (phase C) and V (phase F), fixed for the whole pass
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 63) / 64;
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 63) / 64;
@@ -1123,21 +1127,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
         const int i = e / NX, j = e % NX;
         S.V[e] = rT[rec_off_Lxx(NX) + e] + (i == j ? preg : 0.0);
       }
-      if (l < NX) S.fs[l] = d.fs[((long)b * (N + 1) + N) * NX + l];
+      S.fs[l] = d.fs[((long)b * (N + 1) + N) * NX + (l < NX ? l : NX - 1)];
     }
     lds_sync();
+    // Prefetch of the next node's inputs: unconditional loads from clamped
+    // addresses and unguarded LDS stores, so the code stays straight-line and
+    // the compiler can wait on exactly these loads (a guarded store makes it
+    // wait vmcnt(0), i.e. also on the previous node's K / k / w stores).
+    const int lx = l < NX ? l : NX - 1, lu = l < NU ? l : NU - 1;
     double pf[NPF];
     {
       const double* r1 = recb + (long)(N - 1) * REC;
 #pragma unroll
-      for (int k = 0; k < NPF; ++k) pf[k] = (l + 64 * k < REC) ? r1[l + 64 * k] : 0.0;
+      for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
     }
-    double pfs = (l < NX) ? d.fs[((long)b * (N + 1) + N - 1) * NX + l] : 0.0;
-    double pkp = 0.0, pus = 0.0;
-    if (l < NU) {
-      pkp = d.k[((long)b * N + N - 1) * NU + l];
-      pus = d.us[((long)b * N + N - 1) * NU + l];
-    }
+    double pfs = d.fs[((long)b * (N + 1) + N - 1) * NX + lx];
+    double pkp = d.k[((long)b * N + N - 1) * NU + lu];
+    double pus = d.us[((long)b * N + N - 1) * NU + lu];
     {
       double cdg = 0.0, cdq = 0.0;
       if (l < NX) {
@@ -1160,22 +1166,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
     for (int t = N - 1; t >= 0; --t) {
       // ---- stage record t (prefetched) ; start loading record t-1 ----
 #pragma unroll
-      for (int k = 0; k < NPF; ++k)
-        if (l + 64 * k < REC) S.R[l + 64 * k] = pf[k];
-      if (l < NX) S.fs[l] = pfs;
-      if (l < NU) {
-        S.kp[l] = pkp;
-        S.uu[l] = pus;
-      }
-      if (t > 0) {
-        const double* r1 = recb + (long)(t - 1) * REC;
+      for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
+      S.fs[l] = pfs;
+      S.kp[l] = pkp;
+      S.uu[l] = pus;
+      {
+        const int tn = t > 0 ? t - 1 : 0;
+        const double* r1 = recb + (long)tn * REC;
 #pragma unroll
-        for (int k = 0; k < NPF; ++k) pf[k] = (l + 64 * k < REC) ? r1[l + 64 * k] : 0.0;
-        if (l < NX) pfs = d.fs[((long)b * (N + 1) + t - 1) * NX + l];
-        if (l < NU) {
-          pkp = d.k[((long)b * N + t - 1) * NU + l];
-          pus = d.us[((long)b * N + t - 1) * NU + l];
-        }
+        for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
+        pfs = d.fs[((long)b * (N + 1) + tn) * NX + lx];
+        pkp = d.k[((long)b * N + tn) * NU + lu];
+        pus = d.us[((long)b * N + tn) * NU + lu];
       }
       lds_sync();
       PP(0);
@@ -1225,7 +1227,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
       lds_sync();
       PP(2);
       // ---- phase C: Q lower triangle (mirrored), entries fixed per lane ----
-#pragma unroll 1
+#pragma unroll QC_UNROLL
       for (int k = 0; k < NQL; ++k) {
         if (l + 64 * k < NQE) {
           const int r = qrc[k] >> 8, c = qrc[k] & 255;
@@ -1276,8 +1278,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
         } else {
           const bool v = l < NU;
           const double q = v ? S.Qv[NX + l] : 0.0;
-          const double lb = v ? C.u_lb[l] - S.uu[l] : 0.0;
-          const double ub = v ? C.u_ub[l] - S.uu[l] : 0.0;
+          const double lb = v ? S.ulb[l] - S.uu[l] : 0.0;
+          const double ub = v ? S.uub[l] - S.uu[l] : 0.0;
           double x = v ? S.kp[l] : 0.0;
           int clm = 0;
           ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l);
