@@ -45,6 +45,9 @@ constexpr int FW_BLOCK = 64;
 #ifndef FW_WAVES
 #define FW_WAVES 2
 #endif
+#ifndef PRIMAL_WAVES
+#define PRIMAL_WAVES 1
+#endif
 #ifndef QC_UNROLL
 #define QC_UNROLL 1
 #endif
@@ -128,7 +131,7 @@ struct NodeShared {
 // calc of every node, one lane per node: the primal of calcDiff (dynamics,
 // residuals, activations, cost) plus the node cost, contact force and gap.
 template <int NC, bool FF>
-__global__ __launch_bounds__(64) void k_primal(const DevConsts* __restrict__ Cg, Dev d,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_WAVES))) void k_primal(const DevConsts* __restrict__ Cg, Dev d,
                                                const double* __restrict__ x0,
                                                const double* __restrict__ node_ref,
                                                const double* __restrict__ inst_ref,
@@ -148,8 +151,7 @@ __global__ __launch_bounds__(64) void k_primal(const DevConsts* __restrict__ Cg,
   const double* xreg = inst_ref + (long)b * 21;
   const double* uin = FF ? (y + 14) : (terminal ? nullptr : d.us + ((long)b * N + t) * NU);
   Primal P;
-  node_primal<NC>(C, mode, surf, y, uin, ref, xreg, xreg + 14, P);
-  copy_primal(P, d.prim[node]);
+  node_primal<NC>(C, mode, surf, y, uin, ref, xreg, xreg + 14, P, d.prim + node);
   {
     double acc[NQ];
 #pragma unroll

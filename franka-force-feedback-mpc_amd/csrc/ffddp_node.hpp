@@ -202,7 +202,11 @@ template <int NC> FFD_HD void force_world(const double* lam, double* fw) {
 // ref: p_ref(3), v_ref(3) for this node, xreg (14), tau_ref (7).
 template <int NC>
 FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double* x, const double* u,
-                        const double* ref, const double* xreg, const double* tauref, Primal& P) {
+                        const double* ref, const double* xreg, const double* tauref, Primal& P,
+                        Primal* gout = nullptr) {
+  // gout: each block of fields is stored as soon as it is final, so the
+  // registers holding it can be reused (a whole-struct copy at the end would
+  // keep all ~225 words live to the last instruction).
   constexpr int nc = NC;
   const bool with_dyn = mode != MODE_TERMINAL_X;
   const bool terminal = mode != MODE_RUNNING;
@@ -230,6 +234,19 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   P.pee[2] = K.pee.z;
   #pragma unroll
   for (int k = 0; k < 9; ++k) P.Ree[k] = K.Ree.m[k];
+  if (gout) {
+  #pragma unroll
+    for (int i = 0; i < NQ; ++i)
+  #pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        gout->z[i][k] = P.z[i][k];
+        gout->o[i][k] = P.o[i][k];
+      }
+  #pragma unroll
+    for (int k = 0; k < 3; ++k) gout->pee[k] = P.pee[k];
+  #pragma unroll
+    for (int k = 0; k < 9; ++k) gout->Ree[k] = P.Ree[k];
+  }
   const double pstar[3] = {ref[0], ref[1], ref[2] - C.z_press};
   P.lam[0] = P.lam[1] = P.lam[2] = 0.0;
   if (with_dyn) {
@@ -307,6 +324,23 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
     }
   }
 
+  if (gout) {
+  #pragma unroll
+    for (int i = 0; i < NQ; ++i) gout->a[i] = P.a[i];
+  #pragma unroll
+    for (int i = 0; i < 3; ++i) gout->lam[i] = P.lam[i];
+  #pragma unroll
+    for (int i = 0; i < 28; ++i) gout->L[i] = P.L[i];
+  #pragma unroll
+    for (int r = 0; r < 3; ++r)
+  #pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        gout->Jc[r][i] = P.Jc[r][i];
+        gout->Y[r][i] = P.Y[r][i];
+      }
+  #pragma unroll
+    for (int i = 0; i < 6; ++i) gout->Ls[i] = P.Ls[i];
+  }
   // ---------------- costs (CostModelSum, in _make_dam order) ----------------
   double cost = 0.0;
   #pragma unroll
@@ -483,6 +517,28 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   } else {
     #pragma unroll
     for (int i = 0; i < 14; ++i) P.xnext[i] = x[i];
+  }
+  if (gout) {
+  #pragma unroll
+    for (int i = 0; i < 3; ++i) gout->r_rot[i] = P.r_rot[i];
+    gout->th_rot = P.th_rot;
+  #pragma unroll
+    for (int i = 0; i < NDENSE_MAX; ++i) {
+      gout->D[i] = P.D[i];
+      gout->g[i] = P.g[i];
+    }
+  #pragma unroll
+    for (int i = 0; i < 14; ++i) {
+      gout->Dx[i] = P.Dx[i];
+      gout->gx[i] = P.gx[i];
+      gout->xnext[i] = P.xnext[i];
+    }
+  #pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      gout->Du[i] = P.Du[i];
+      gout->gu[i] = P.gu[i];
+    }
+    gout->cost = P.cost;
   }
 }
 
