@@ -115,3 +115,20 @@ def test_solve_variants_match_oracle(box, regime):
         assert rel_err(solver.xs[i], s.xs) < TOL_SOLVE
         assert rel_err(solver.us[i], s.us) < TOL_SOLVE
         assert rel_err(solver.K[i], s.K) < TOL_SOLVE * 10
+
+
+def test_long_horizon_point3d_matches_oracle():
+    """BASELINE config 5 shape: horizon 100, point3d contact, maxiter 10."""
+    N, B = 100, 2
+    cfg = product_cfg("classical", N, "point3d")
+    b = make_batch("classical", B, N, seed=55, surface=1)
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    ok = solver.solve(b, maxiter=10, is_feasible=False)
+    for i in range(B):
+        ok_o, s = oracle_solve(cfg, b, i)
+        assert bool(ok[i]) == bool(ok_o)
+        assert int(solver.iter[i]) == int(s.iter), (i, solver.iter[i], s.iter)
+        assert rel_err(solver.cost[i], s.cost) < TOL_SOLVE
+        assert rel_err(solver.xs[i], s.xs) < TOL_SOLVE
+        assert rel_err(solver.us[i], s.us) < TOL_SOLVE
+        assert rel_err(solver.K[i], s.K) < TOL_SOLVE * 10
