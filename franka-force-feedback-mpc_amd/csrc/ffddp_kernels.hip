@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -1803,6 +1804,99 @@ __global__ __launch_bounds__(64) void k_gravity(const ffddp_robot* __restrict__ 
   gravity_torque(*rb, q + (long)b * NQ, tau + (long)b * NQ);
 }
 
+// ---------------------------------------------------------------------------
+// Problem builder (ffddp_build_problem_dev): one thread per (instance, knot).
+// make_approach_then_circle (trajectories.py:8-93) + the benchmark hold
+// (run_classical.py:256-264), MuJoCo -> Pinocchio (crocoddyl_classical.py:
+// 250-258, R_MJ_FROM_PIN = diag(-1,-1,1)), references (:447-466).
+// ---------------------------------------------------------------------------
+struct TaskTraj {
+  double center[3], radius, omega, z_contact, t_approach, t_pre, t_hold;
+  double p_start[3], p_pre[3], p_cs[3];
+};
+
+__device__ __forceinline__ double smoothstep01(double s) {
+  s = fmin(fmax(s, 0.0), 1.0);
+  return s * s * (3.0 - 2.0 * s);
+}
+
+__device__ __forceinline__ double dsmoothstep01(double s) {
+  s = fmin(fmax(s, 0.0), 1.0);
+  return 6.0 * s * (1.0 - s);
+}
+
+// base(t) -> (p, v, surface) in the MuJoCo world
+__device__ bool task_base(const TaskTraj& T, double t, double p[3], double v[3]) {
+  const double* p0;
+  const double* p1;
+  double tau, dur;
+  if (T.t_pre > 0.0 && t < T.t_pre) {
+    p0 = T.p_start; p1 = T.p_pre; tau = t; dur = T.t_pre;
+  } else if (t < T.t_pre + T.t_approach) {
+    p0 = T.t_pre > 0.0 ? T.p_pre : T.p_start; p1 = T.p_cs; tau = t - T.t_pre; dur = T.t_approach;
+  } else {
+    const double th = T.omega * (t - (T.t_pre + T.t_approach));
+    double sn, cs;
+    sincos(th, &sn, &cs);
+    p[0] = T.center[0] + T.radius * cs;
+    p[1] = T.center[1] + T.radius * sn;
+    p[2] = T.z_contact;
+    v[0] = -T.radius * T.omega * sn;
+    v[1] = T.radius * T.omega * cs;
+    v[2] = 0.0;
+    return true;
+  }
+  const double sl = tau / dur, s = smoothstep01(sl), dsdt = dsmoothstep01(sl) / dur;
+  for (int i = 0; i < 3; ++i) {
+    p[i] = (1.0 - s) * p0[i] + s * p1[i];
+    v[i] = dsdt * (p1[i] - p0[i]);
+  }
+  return false;
+}
+
+__device__ bool task_eval(const TaskTraj& T, double t, double p[3], double v[3]) {
+  const bool surf = task_base(T, t, p, v);
+  const double tc = T.t_pre + T.t_approach;
+  if (surf && t < tc + T.t_hold) {
+    double vh[3];
+    task_base(T, tc, p, vh);
+    v[0] = v[1] = v[2] = 0.0;
+  }
+  return surf;
+}
+
+__global__ __launch_bounds__(64) void k_build(const ffddp_robot* __restrict__ rb, TaskTraj T, ffddp_task task, int B,
+                                              int N, int nx, double dt, const double* __restrict__ t0,
+                                              const double* __restrict__ x0, double* __restrict__ node_ref,
+                                              double* __restrict__ inst_ref, uint8_t* __restrict__ surface) {
+  const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long)B * (N + 1)) return;
+  const int b = (int)(g / (N + 1)), k = (int)(g - (long)b * (N + 1));
+  double p[3], v[3];
+  task_eval(T, t0[b] + k * dt, p, v);
+  double* o = node_ref + g * 6;
+  o[0] = -p[0] - task.p_site_minus_frame[0];
+  o[1] = -p[1] - task.p_site_minus_frame[1];
+  o[2] = p[2] - task.p_site_minus_frame[2];
+  o[3] = -v[0];
+  o[4] = -v[1];
+  o[5] = v[2];
+  if (k != 0) return;
+  double pp[3], vv[3];
+  surface[b] = task_eval(T, t0[b], pp, vv) ? 1 : 0;
+  const double* xb = x0 + (long)b * nx;
+  double* ir = inst_ref + (long)b * 21;
+  for (int i = 0; i < 7; ++i) {
+    ir[i] = task.posture_mode ? task.q_nom[i] : xb[i];
+    ir[7 + i] = task.posture_mode ? 0.0 : xb[7 + i];
+  }
+  if (task.torque_mode == 2) {
+    for (int i = 0; i < 7; ++i) ir[14 + i] = 0.0;
+  } else {
+    gravity_torque(*rb, task.torque_mode == 1 ? task.q_nom : xb, ir + 14);
+  }
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -2477,6 +2571,41 @@ int ffddp_gravity_torque_dev(ffddp_handle* h, int B, const double* q, double* ta
   if (B == 0) return 0;
   HIPCHK(h, hipSetDevice(h->device));
   hipLaunchKernelGGL(k_gravity, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, h->drb, B, q, tau);
+  HIPCHK(h, hipGetLastError());
+  return 0;
+}
+
+int ffddp_build_problem_dev(ffddp_handle* h, int B, const ffddp_task* task, const double* t0, const double* x0,
+                            double* node_ref, double* inst_ref, uint8_t* surface, void* stream) {
+  if (!h || !task || B < 0) return FFDDP_E_INVALID;
+  if (B == 0) return 0;
+  if (!t0 || !x0 || !node_ref || !inst_ref || !surface) return FFDDP_E_INVALID;
+  if (task->posture_mode < 0 || task->posture_mode > 1 || task->torque_mode < 0 || task->torque_mode > 2) {
+    h->err = "ffddp_build_problem_dev: posture_mode must be 0/1 and torque_mode 0/1/2";
+    return FFDDP_E_INVALID;
+  }
+  // make_approach_then_circle's closure constants (trajectories.py:36-60)
+  TaskTraj T{};
+  for (int i = 0; i < 3; ++i) T.center[i] = task->center[i];
+  T.radius = task->radius;
+  T.omega = task->omega;
+  T.z_contact = task->z_contact;
+  T.t_approach = std::max(task->t_approach, 1.0e-6);
+  T.t_pre = std::max(task->t_pre, 0.0);
+  T.t_hold = task->t_hold;
+  for (int i = 0; i < 3; ++i) T.p_cs[i] = task->center[i];
+  T.p_cs[0] += task->radius;
+  T.p_cs[2] = task->z_contact;
+  for (int i = 0; i < 3; ++i) T.p_start[i] = task->has_ee_start ? task->ee_start[i] : T.p_cs[i];
+  if (!task->has_ee_start) T.p_start[2] += 0.08;
+  const double z_pre = task->has_z_pre ? task->z_pre : std::max(task->z_contact + 0.05, T.p_start[2]);
+  for (int i = 0; i < 3; ++i) T.p_pre[i] = T.p_cs[i];
+  T.p_pre[2] = z_pre;
+  const int N = h->hc.N;
+  const long n = (long)B * (N + 1);
+  HIPCHK(h, hipSetDevice(h->device));
+  hipLaunchKernelGGL(k_build, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, h->drb, T, *task, B, N,
+                     h->hc.nx, h->hc.dt, t0, x0, node_ref, inst_ref, surface);
   HIPCHK(h, hipGetLastError());
   return 0;
 }

@@ -29,6 +29,7 @@ SYMBOLS = (
     "ffddp_frame_placement",
     "ffddp_gravity_torque",
     "ffddp_gravity_torque_dev",
+    "ffddp_build_problem_dev",
     "ffddp_profile_enable",
     "ffddp_profile_read",
 )
@@ -92,6 +93,69 @@ class OcpConfig(C.Structure):
         ("use_inner_state_reg", C.c_int32),
         ("use_inner_tau_reg", C.c_int32),
     ]
+
+
+class Task(C.Structure):
+    """ffddp_task: the device problem builder's task (trajectories.py:8-93,
+    run_classical.py:221-264, crocoddyl_classical.py:250-258, 447-466)."""
+
+    _fields_ = [
+        ("center", C.c_double * 3),
+        ("radius", C.c_double),
+        ("omega", C.c_double),
+        ("z_contact", C.c_double),
+        ("t_approach", C.c_double),
+        ("t_pre", C.c_double),
+        ("z_pre", C.c_double),
+        ("t_hold", C.c_double),
+        ("ee_start", C.c_double * 3),
+        ("has_ee_start", C.c_int32),
+        ("has_z_pre", C.c_int32),
+        ("p_site_minus_frame", C.c_double * 3),
+        ("q_nom", C.c_double * 7),
+        ("posture_mode", C.c_int32),
+        ("torque_mode", C.c_int32),
+    ]
+
+
+POSTURE_MODES = {"x0": 0, "q_nom": 1}
+TORQUE_MODES = {"gravity_x0": 0, "gravity_q_nom": 1, "zero": 2}
+
+
+def make_task(
+    center,
+    radius: float,
+    omega: float,
+    z_contact: float,
+    t_approach: float = 2.0,
+    ee_start=None,
+    z_pre=None,
+    t_pre: float = 0.0,
+    t_hold: float = 0.0,
+    p_site_minus_frame=(0.0, 0.0, 0.0),
+    q_nom=None,
+    posture_ref_mode: str = "q_nom",
+    torque_ref_mode: str = "gravity_x0",
+) -> Task:
+    """Task with make_approach_then_circle's arguments (trajectories.py:8-17),
+    the benchmark hold t_hold (run_classical.py:256-264: 0.2 s) and the
+    controller's reference modes (crocoddyl_classical.py:447-466)."""
+    t = Task()
+    _fill(t.center, center)
+    t.radius, t.omega, t.z_contact = float(radius), float(omega), float(z_contact)
+    t.t_approach, t.t_pre, t.t_hold = float(t_approach), float(t_pre), float(t_hold)
+    t.has_ee_start = int(ee_start is not None)
+    if ee_start is not None:
+        _fill(t.ee_start, ee_start)
+    t.has_z_pre = int(z_pre is not None)
+    t.z_pre = float(z_pre) if z_pre is not None else 0.0
+    _fill(t.p_site_minus_frame, p_site_minus_frame)
+    _fill(t.q_nom, R.Q_NEUTRAL if q_nom is None else q_nom)
+    if posture_ref_mode not in POSTURE_MODES or torque_ref_mode not in TORQUE_MODES:
+        raise ValueError(f"unknown reference mode {posture_ref_mode!r} / {torque_ref_mode!r}")
+    t.posture_mode = POSTURE_MODES[posture_ref_mode]
+    t.torque_mode = TORQUE_MODES[torque_ref_mode]
+    return t
 
 
 def _fill(arr, values):
@@ -158,6 +222,8 @@ def load() -> C.CDLL:
     lib.ffddp_gravity_torque.restype = C.c_int
     lib.ffddp_gravity_torque_dev.argtypes = [C.c_void_p, C.c_int, vp, vp, vp]
     lib.ffddp_gravity_torque_dev.restype = C.c_int
+    lib.ffddp_build_problem_dev.argtypes = [C.c_void_p, C.c_int, C.POINTER(Task)] + [vp] * 6
+    lib.ffddp_build_problem_dev.restype = C.c_int
     lib.ffddp_profile_enable.argtypes = [C.c_void_p, C.c_int]
     lib.ffddp_profile_enable.restype = C.c_int
     lib.ffddp_profile_read.argtypes = [C.c_void_p, dp, C.POINTER(C.c_int64), C.c_int]

@@ -104,6 +104,20 @@ class BatchedBoxFDDP:
         )
         self._check(rc, "ffddp_solve_batch_dev")
 
+    # -- device-side problem builder ----------------------------------------------
+    def build_problem_dev(self, task, t, stream=None):
+        """Fill t["node_ref"], t["inst_ref"], t["surface"] on the device from
+        t["t0"] (B,) and t["x0"] (B, nx) for `task` (_abi.Task / make_task):
+        _build_problem's references (crocoddyl_classical.py:521-556) for B
+        instances in one launch.  Asynchronous on `stream`."""
+        B = int(t["x0"].shape[0])
+        p = lambda k: C.c_void_p(int(t[k].data_ptr()))
+        rc = self._lib.ffddp_build_problem_dev(
+            self._h, B, C.byref(task), p("t0"), p("x0"), p("node_ref"), p("inst_ref"), p("surface"),
+            C.c_void_p(stream if stream else 0),
+        )
+        self._check(rc, "ffddp_build_problem_dev")
+
     # -- per-kernel device timing ----------------------------------------------------
     def profile(self, on=True):
         """on: True (every kernel class), False, or an iterable of class names

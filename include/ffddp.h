@@ -91,6 +91,24 @@ typedef struct ffddp_ocp_config {
   int32_t use_inner_state_reg, use_inner_tau_reg;
 } ffddp_ocp_config;
 
+/* Task description for the device-side problem builder:
+ * the approach-then-circle EE reference of src/tasks/trajectories.py:8-93
+ * with the benchmark runner's contact-onset hold (run_classical.py:221-264),
+ * the MuJoCo->Pinocchio target mapping (crocoddyl_classical.py:250-258) and
+ * the posture / torque reference modes (crocoddyl_classical.py:447-466). */
+typedef struct ffddp_task {
+  double center[3];   /* circle centre, MuJoCo world (z = contact height) */
+  double radius, omega, z_contact, t_approach, t_pre;
+  double z_pre;       /* used when has_z_pre, else max(z_contact + 0.05, ee_start z) */
+  double t_hold;      /* benchmark hold at contact onset (0.2 s; 0 = none) */
+  double ee_start[3]; /* used when has_ee_start, else contact start + (0, 0, 0.08) */
+  int32_t has_ee_start, has_z_pre;
+  double p_site_minus_frame[3]; /* _calibrate_site_position_offset (Pinocchio frame) */
+  double q_nom[7];
+  int32_t posture_mode; /* 0: x_reg_ref = x0[:14]; 1: [q_nom, 0] */
+  int32_t torque_mode;  /* 0: gravity(x0 q); 1: gravity(q_nom); 2: zero */
+} ffddp_task;
+
 typedef struct ffddp_handle ffddp_handle;
 
 /* crocoddyl.SolverBoxFDDP(problem) / setProblem (crocoddyl_classical.py:350-361):
@@ -164,6 +182,17 @@ int ffddp_profile_read(ffddp_handle* h, double* ms, int64_t* launches, int reset
 
 /* Batched gravity torque on the device (tau_ref for B instances), device pointers. */
 int ffddp_gravity_torque_dev(ffddp_handle* h, int B, const double* q, double* tau, void* stream);
+
+/* Device-side problem builder: what _build_problem (crocoddyl_classical.py:
+ * 521-556; FF :776-836) feeds the action models, for B instances at once,
+ * as the solver's input arrays.  Instance b solves from time t0[b] and state
+ * x0[b] (nx): knot k samples the task at t0 + k dt_ocp (k = 0..N) and maps
+ * it to the Pinocchio frame; surface[b] = the task's contact flag at t0
+ * (phase_source "trajectory"); inst_ref = posture and torque references.
+ * Device pointers: t0[B], x0[B][nx] -> node_ref[B][N+1][6],
+ * inst_ref[B][21], surface[B]. */
+int ffddp_build_problem_dev(ffddp_handle* h, int B, const ffddp_task* task, const double* t0, const double* x0,
+                            double* node_ref, double* inst_ref, uint8_t* surface, void* stream);
 
 #ifdef __cplusplus
 }

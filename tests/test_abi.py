@@ -36,9 +36,11 @@ def test_struct_layout_matches_header():
 #include <stddef.h>
 #include "ffddp.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(ffddp_robot), sizeof(ffddp_ocp_config),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(ffddp_robot), sizeof(ffddp_ocp_config),
          offsetof(ffddp_ocp_config, dt), offsetof(ffddp_ocp_config, R_des),
-         offsetof(ffddp_ocp_config, y_weights), offsetof(ffddp_ocp_config, use_inner_tau_reg));
+         offsetof(ffddp_ocp_config, y_weights), offsetof(ffddp_ocp_config, use_inner_tau_reg),
+         sizeof(ffddp_task), offsetof(ffddp_task, has_ee_start), offsetof(ffddp_task, q_nom),
+         offsetof(ffddp_task, torque_mode));
   return 0;
 }'''
     with tempfile.TemporaryDirectory() as d:
@@ -50,7 +52,8 @@ int main(void) {
     C = _abi.OcpConfig
     assert vals == [
         ctypes.sizeof(_abi.Robot), ctypes.sizeof(C), C.dt.offset, C.R_des.offset, C.y_weights.offset,
-        C.use_inner_tau_reg.offset,
+        C.use_inner_tau_reg.offset, ctypes.sizeof(_abi.Task), _abi.Task.has_ee_start.offset, _abi.Task.q_nom.offset,
+        _abi.Task.torque_mode.offset,
     ]
 
 
