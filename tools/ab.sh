@@ -12,6 +12,6 @@ for cfg in "$@"; do
 import json,sys
 l=[x for x in open("gpurun_out/ab_bench.log") if x.startswith("{")][-1]
 j=json.loads(l)
-print(sys.argv[1], "value %.0f" % j["value"], "ms %.2f" % j["ms_per_step"], " ".join("%s=%.2f" % (k, v["ms_per_step"]) for k, v in (j["kernels"] or {}).items()), "ok=%.3f it=%.2f" % (j["solver"]["ok_frac"], j["solver"]["mean_iter"]))
+print(sys.argv[1], "value %.0f" % j["value"], "ms %.2f" % j["ms_per_step"], " ".join("%s=%.2f" % (k, v["ms_per_solve"]) for k, v in (j["kernels"] or {}).items()), "ok=%.3f it=%.2f" % (j["solver"]["ok_frac"], j["solver"]["mean_iter"]))
 PY
 done
