@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "ffddp_group.hpp"
+#include "ffddp_plant.hpp"
 
 using namespace ffddp;
 
@@ -1797,6 +1798,29 @@ __global__ __launch_bounds__(64) void k_finalize(const DevConsts* __restrict__ C
   fn_pred[(long)b * 2 + knot] = (NC == 1) ? P.lam[0] : P.lam[2];
 }
 
+// closed-loop plant stand-in: one thread per instance (ffddp_plant.hpp)
+__global__ __launch_bounds__(64) void k_plant(const ffddp_robot* __restrict__ rb, const ffddp_plant_params* __restrict__ pp,
+                                              int B, double* __restrict__ q, double* __restrict__ v,
+                                              const double* __restrict__ tau, const double* __restrict__ plane,
+                                              int integrate, double* __restrict__ obs, int32_t* __restrict__ fail) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double qb[NQ], vb[NQ], tb[NQ], ob[PO_WORDS];
+  for (int i = 0; i < NQ; ++i) {
+    qb[i] = q[(long)b * NQ + i];
+    vb[i] = v[(long)b * NQ + i];
+    tb[i] = tau[(long)b * NQ + i];
+  }
+  const double* pl = plane + (long)b * 6;
+  const bool ok = plant_step(*rb, *pp, qb, vb, tb, pl, pl + 3, integrate, ob);
+  for (int i = 0; i < NQ; ++i) {
+    q[(long)b * NQ + i] = qb[i];
+    v[(long)b * NQ + i] = vb[i];
+  }
+  for (int e = 0; e < PO_WORDS; ++e) obs[(long)b * PO_WORDS + e] = ob[e];
+  if (fail) fail[b] = ok ? 0 : 1;
+}
+
 __global__ __launch_bounds__(64) void k_gravity(const ffddp_robot* __restrict__ rb, int B, const double* __restrict__ q,
                           double* __restrict__ tau) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2607,6 +2631,94 @@ int ffddp_build_problem_dev(ffddp_handle* h, int B, const ffddp_task* task, cons
   hipLaunchKernelGGL(k_build, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, h->drb, T, *task, B, N,
                      h->hc.nx, h->hc.dt, t0, x0, node_ref, inst_ref, surface);
   HIPCHK(h, hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// plant stand-in
+// ---------------------------------------------------------------------------
+struct ffddp_plant {
+  int device = 0, max_batch = 0;
+  ffddp_robot* drb = nullptr;
+  ffddp_plant_params* dpp = nullptr;
+  double *q = nullptr, *v = nullptr, *tau = nullptr, *plane = nullptr, *obs = nullptr;
+  int32_t* fail = nullptr;
+};
+
+extern "C" {
+
+int ffddp_plant_create(const ffddp_robot* robot, const ffddp_plant_params* p, int device, int max_batch,
+                       ffddp_plant** out) {
+  static_assert(PO_WORDS == FFDDP_PLANT_OBS, "plant observation layout");
+  if (!robot || !p || !out || max_batch < 1 || p->timestep <= 0.0 || p->n_substeps < 1) return FFDDP_E_INVALID;
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return FFDDP_E_DEVICE;
+  ffddp_plant* h = new (std::nothrow) ffddp_plant();
+  if (!h) return FFDDP_E_OOM;
+  h->device = device;
+  h->max_batch = max_batch;
+  const size_t B = (size_t)max_batch;
+  bool bad_alloc = hipMalloc((void**)&h->drb, sizeof(ffddp_robot)) != hipSuccess;
+  bad_alloc |= hipMalloc((void**)&h->dpp, sizeof(ffddp_plant_params)) != hipSuccess;
+  bad_alloc |= hipMalloc((void**)&h->q, B * NQ * 8) != hipSuccess;
+  bad_alloc |= hipMalloc((void**)&h->v, B * NQ * 8) != hipSuccess;
+  bad_alloc |= hipMalloc((void**)&h->tau, B * NQ * 8) != hipSuccess;
+  bad_alloc |= hipMalloc((void**)&h->plane, B * 6 * 8) != hipSuccess;
+  bad_alloc |= hipMalloc((void**)&h->obs, B * PO_WORDS * 8) != hipSuccess;
+  bad_alloc |= hipMalloc((void**)&h->fail, B * 4) != hipSuccess;
+  if (bad_alloc || hipMemcpy(h->drb, robot, sizeof(ffddp_robot), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->dpp, p, sizeof(ffddp_plant_params), hipMemcpyHostToDevice) != hipSuccess) {
+    ffddp_plant_destroy(h);
+    return bad_alloc ? FFDDP_E_OOM : FFDDP_E_DEVICE;
+  }
+  *out = h;
+  return 0;
+}
+
+void ffddp_plant_destroy(ffddp_plant* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  void* ps[] = {h->drb, h->dpp, h->q, h->v, h->tau, h->plane, h->obs, h->fail};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  delete h;
+}
+
+int ffddp_plant_step_dev(ffddp_plant* h, int B, double* q, double* v, const double* tau, const double* plane,
+                         int integrate, double* obs, int32_t* fail, void* stream) {
+  if (!h || B < 0 || B > h->max_batch) return FFDDP_E_INVALID;
+  if (B == 0) return 0;
+  if (!q || !v || !tau || !plane || !obs) return FFDDP_E_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return FFDDP_E_DEVICE;
+  hipLaunchKernelGGL(k_plant, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, h->drb, h->dpp, B, q, v, tau,
+                     plane, integrate, obs, fail);
+  return hipGetLastError() == hipSuccess ? 0 : FFDDP_E_DEVICE;
+}
+
+int ffddp_plant_step(ffddp_plant* h, int B, double* q, double* v, const double* tau, const double* plane,
+                     int integrate, double* obs) {
+  if (!h || B < 0 || B > h->max_batch) return FFDDP_E_INVALID;
+  if (B == 0) return 0;
+  if (!q || !v || !tau || !plane || !obs) return FFDDP_E_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return FFDDP_E_DEVICE;
+  const size_t n7 = (size_t)B * NQ * 8;
+  if (hipMemcpy(h->q, q, n7, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->v, v, n7, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->tau, tau, n7, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->plane, plane, (size_t)B * 6 * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return FFDDP_E_DEVICE;
+  int rc = ffddp_plant_step_dev(h, B, h->q, h->v, h->tau, h->plane, integrate, h->obs, h->fail, nullptr);
+  if (rc) return rc;
+  std::vector<int32_t> fl((size_t)B);
+  if (hipMemcpy(q, h->q, n7, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(v, h->v, n7, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(obs, h->obs, (size_t)B * PO_WORDS * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(fl.data(), h->fail, (size_t)B * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return FFDDP_E_DEVICE;
+  for (int b = 0; b < B; ++b)
+    if (fl[b]) return FFDDP_E_INVALID;
   return 0;
 }
 

@@ -32,7 +32,12 @@ SYMBOLS = (
     "ffddp_build_problem_dev",
     "ffddp_profile_enable",
     "ffddp_profile_read",
+    "ffddp_plant_create",
+    "ffddp_plant_destroy",
+    "ffddp_plant_step",
+    "ffddp_plant_step_dev",
 )
+PLANT_OBS = 69
 NSTATS = 6
 KERNEL_CLASSES = ("init", "node", "backward", "forward", "accept", "commit", "finalize")
 
@@ -115,6 +120,22 @@ class Task(C.Structure):
         ("q_nom", C.c_double * 7),
         ("posture_mode", C.c_int32),
         ("torque_mode", C.c_int32),
+    ]
+
+
+class PlantParams(C.Structure):
+    """ffddp_plant_params: the closed-loop plant stand-in (ffddp_plant.hpp)."""
+
+    _fields_ = [
+        ("timestep", C.c_double),
+        ("n_substeps", C.c_int32),
+        ("armature", C.c_double * 7),
+        ("damping", C.c_double * 7),
+        ("r_tool", C.c_double),
+        ("margin", C.c_double),
+        ("solref", C.c_double * 2),
+        ("solimp", C.c_double * 5),
+        ("site_R", C.c_double * 2),
     ]
 
 
@@ -228,6 +249,15 @@ def load() -> C.CDLL:
     lib.ffddp_profile_enable.restype = C.c_int
     lib.ffddp_profile_read.argtypes = [C.c_void_p, dp, C.POINTER(C.c_int64), C.c_int]
     lib.ffddp_profile_read.restype = C.c_int
+    lib.ffddp_plant_create.argtypes = [C.POINTER(Robot), C.POINTER(PlantParams), C.c_int, C.c_int,
+                                       C.POINTER(C.c_void_p)]
+    lib.ffddp_plant_create.restype = C.c_int
+    lib.ffddp_plant_destroy.argtypes = [C.c_void_p]
+    lib.ffddp_plant_destroy.restype = None
+    lib.ffddp_plant_step.argtypes = [C.c_void_p, C.c_int, dp, dp, dp, dp, C.c_int, dp]
+    lib.ffddp_plant_step.restype = C.c_int
+    lib.ffddp_plant_step_dev.argtypes = [C.c_void_p, C.c_int] + [vp] * 4 + [C.c_int, vp, vp, vp]
+    lib.ffddp_plant_step_dev.restype = C.c_int
     _lib = lib
     return lib
 

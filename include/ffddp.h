@@ -194,8 +194,44 @@ int ffddp_gravity_torque_dev(ffddp_handle* h, int B, const double* q, double* ta
 int ffddp_build_problem_dev(ffddp_handle* h, int B, const ffddp_task* task, const double* t0, const double* x0,
                             double* node_ref, double* inst_ref, uint8_t* surface, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Closed-loop plant stand-in: the MuJoCo plant of the
+ * reference's closed loop, FrankaMujocoSim.step() in torque mode
+ * (src/sim/franka_sim.py:144-169) on assets/scenes/panda_table_scene.xml:
+ * arm (+ joint armature / damping, panda_robot.xml:9), tool sphere at the
+ * ee_site (:189-199) against the table_contact plane (condim 1, soft
+ * constraint solref/solimp), implicitfast integration, n_substeps physics
+ * steps per control step.  Observation record: FFDDP_PLANT_OBS words per
+ * instance (q, dq, qfrc_bias, qfrc_constraint, site pos/vel/rot, contact force,
+ * site Jacobian), see ffddp_plant.hpp.  Parity with MuJoCo is unpinned.
+ * ------------------------------------------------------------------------- */
+#define FFDDP_PLANT_OBS 69
+typedef struct ffddp_plant_params {
+  double timestep;      /* model.opt.timestep (benchmark protocol: 0.001) */
+  int32_t n_substeps;   /* physics steps per control step (5) */
+  double armature[7], damping[7];
+  double r_tool;        /* ee_collision sphere radius (0.03) */
+  double margin;        /* contact margin (0.001) */
+  double solref[2];     /* (timeconst, dampratio), MuJoCo default (0.02, 1) */
+  double solimp[5];     /* MuJoCo default (0.9, 0.95, 0.001, 0.5, 2) */
+  double site_R[2];     /* cos, sin of the tool-body yaw (135 deg) */
+} ffddp_plant_params;
+
+typedef struct ffddp_plant ffddp_plant;
+int ffddp_plant_create(const ffddp_robot* robot, const ffddp_plant_params* p, int device, int max_batch,
+                       ffddp_plant** out);
+void ffddp_plant_destroy(ffddp_plant* h);
+/* One control step of B plants (integrate = 0: forward only, like mj_forward).
+ * Host pointers: q, v [B][7] (in/out), tau [B][7] applied torque, plane [B][6]
+ * = table normal (3) and a point on the plane (3), MuJoCo world; obs
+ * [B][FFDDP_PLANT_OBS].  Returns FFDDP_E_INVALID on a non-SPD mass matrix. */
+int ffddp_plant_step(ffddp_plant* h, int B, double* q, double* v, const double* tau, const double* plane,
+                     int integrate, double* obs);
+/* Same on device pointers, asynchronous on `stream` (per-instance failure flags in fail[B], may be NULL). */
+int ffddp_plant_step_dev(ffddp_plant* h, int B, double* q, double* v, const double* tau, const double* plane,
+                         int integrate, double* obs, int32_t* fail, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
-
 #endif /* FFDDP_H_ */

@@ -36,6 +36,8 @@ def test_struct_layout_matches_header():
 #include <stddef.h>
 #include "ffddp.h"
 int main(void) {
+  printf("%zu %zu %zu %zu %d ", sizeof(ffddp_plant_params), offsetof(ffddp_plant_params, armature),
+         offsetof(ffddp_plant_params, r_tool), offsetof(ffddp_plant_params, site_R), FFDDP_PLANT_OBS);
   printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(ffddp_robot), sizeof(ffddp_ocp_config),
          offsetof(ffddp_ocp_config, dt), offsetof(ffddp_ocp_config, R_des),
          offsetof(ffddp_ocp_config, y_weights), offsetof(ffddp_ocp_config, use_inner_tau_reg),
@@ -50,6 +52,9 @@ int main(void) {
         subprocess.run(["gcc", "-I", str(ROOT / "include"), str(c), "-o", str(exe)], check=True)
         vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     C = _abi.OcpConfig
+    Pp = _abi.PlantParams
+    assert vals[:5] == [ctypes.sizeof(Pp), Pp.armature.offset, Pp.r_tool.offset, Pp.site_R.offset, _abi.PLANT_OBS]
+    vals = vals[5:]
     assert vals == [
         ctypes.sizeof(_abi.Robot), ctypes.sizeof(C), C.dt.offset, C.R_des.offset, C.y_weights.offset,
         C.use_inner_tau_reg.offset, ctypes.sizeof(_abi.Task), _abi.Task.has_ee_start.offset, _abi.Task.q_nom.offset,
