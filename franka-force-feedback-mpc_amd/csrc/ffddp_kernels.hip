@@ -1503,8 +1503,11 @@ __global__ __launch_bounds__(FW_BLOCK) void k_forward(const DevConsts* __restric
 // joint-parallel (node_calc_g8), which shortens the dependent chain that
 // bounds this kernel.  Lane i < 7 carries joint i of x (q_i, v_i, FF tau_i).
 // ---------------------------------------------------------------------------
-template <int NC, bool FF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) void k_forward_g8(const DevConsts* __restrict__ Cg, Dev d,
+// W: waves/SIMD occupancy target (2 while the batch is throughput-bound, 1 for
+// the latency-bound late iterations, where the register budget also holds the
+// next node's K row: PK = prefetch it one node ahead)
+template <int NC, bool FF, int W = FW_WAVES, bool PK = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_forward_g8(const DevConsts* __restrict__ Cg, Dev d,
                                                    const double* __restrict__ x0,
                                                    const double* __restrict__ node_ref,
                                                    const double* __restrict__ inst_ref,
@@ -1558,11 +1561,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) 
       const long ub = (long)b * N + t;
       pus = J ? d.us[ub * NU + ji] : 0.0;
       pk = J ? d.k[ub * NU + ji] : 0.0;
-#ifdef FW_PREFETCH_K
-      const double* K_t = d.K + ub * NU * nx + (long)ji * nx;
+      if constexpr (PK) {
+        const double* K_t = d.K + ub * NU * nx + (long)ji * nx;
 #pragma unroll
-      for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
-#endif
+        for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
+      }
     }
   };
   fetch(0);
@@ -1587,11 +1590,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FW_WAVES))) 
       // u_i = us_i - alpha k_i - K_i (x - xs)
       double u = 0.0;
       {
-#ifndef FW_PREFETCH_K
-        const double* K_t = d.K + ((long)b * N + t) * NU * nx + (long)ji * nx;
+        if constexpr (!PK) {
+          const double* K_t = d.K + ((long)b * N + t) * NU * nx + (long)ji * nx;
 #pragma unroll
-        for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
-#endif
+          for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
+        }
         double acc = pus - pk * alpha;
         const double dq = xq_t - sq, dv = xv_t - sv, dtt = xt_t - stt;
 #pragma unroll
@@ -1949,6 +1952,8 @@ struct ffddp_handle {
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
   bool bw_wave = true;
   int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
+  int fw_first0 = 2;  // same for iteration 0 (FFDDP_FW_FIRST0)
+  int fw_late_it = 0;  // first iteration using the 1-wave/SIMD line-search variant (FFDDP_FW_LATE_IT)
   bool fw_group = true;  // 8-lane joint-parallel line search; FFDDP_FW=lane selects one lane per trial  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
   // optional per-kernel timing
   bool prof = false;
@@ -2232,13 +2237,23 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       {
         ProfScope p(h, ss, KC_FORWARD);
         if (h->fw_group) {
-          const int n1 = h->fw_first;
-          hipLaunchKernelGGL((k_forward_g8<NC, FF>), dim3((int)(((long)Bk * n1 * G8 + 63) / 64)), dim3(64), 0, ss, h->dc,
-                             d, x0k, nrefk, irefk, surfk, 0, n1, 0);
+          // first pass: trials 0..n1-1; iteration 0 of a cold start almost
+          // always accepts alpha = 1 or 1/2 (fw_first0), later ones up to 1/8
+          const int n1 = it == 0 ? h->fw_first0 : h->fw_first;
+          const bool late = it >= h->fw_late_it;
+          auto fw = [&](int tr0, int ntr, int more) {
+            const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
+            if (late)
+              hipLaunchKernelGGL((k_forward_g8<NC, FF, 1, true>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
+                                 surfk, tr0, ntr, more);
+            else
+              hipLaunchKernelGGL((k_forward_g8<NC, FF>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk,
+                                 tr0, ntr, more);
+          };
+          fw(0, n1, 0);
           if (n1 < NTRIALS) {
             hipLaunchKernelGGL(k_probe, dim3((Bk + 255) / 256), dim3(256), 0, ss, h->dc, d, n1);
-            hipLaunchKernelGGL((k_forward_g8<NC, FF>), dim3((int)(((long)Bk * (NTRIALS - n1) * G8 + 63) / 64)),
-                               dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk, n1, NTRIALS - n1, 1);
+            fw(n1, NTRIALS - n1, 1);
           }
         } else {
           hipLaunchKernelGGL((k_forward<NC, FF>), dim3((int)(((long)Bk * NTRIALS + FW_BLOCK - 1) / FW_BLOCK)),
@@ -2347,6 +2362,11 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     }
     const char* fw = std::getenv("FFDDP_FW");
     h->fw_group = !(fw && std::strcmp(fw, "lane") == 0);
+    if (const char* f0 = std::getenv("FFDDP_FW_FIRST0")) {
+      const int v = std::atoi(f0);
+      h->fw_first0 = v < 1 ? 1 : (v > NTRIALS ? NTRIALS : v);
+    }
+    if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
     const char* f1 = std::getenv("FFDDP_FW_FIRST");
     if (f1) {
       const int v = std::atoi(f1);
