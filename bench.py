@@ -13,7 +13,8 @@ Prints ONE JSON line (rank 0).  Extra objects:
   roofline      dominant kernel's algorithmic bytes per launch / its average
                 HIP-event-timed launch duration, vs 8 TB/s.
   cpu_baseline  the numpy oracle (oracle/, the CPU restatement) timed on a
-                bounded sample of the same workload on one host core.
+                bounded sample of the same workload on the host cores (one
+                worker process per core, up to 16), in a child process.
 """
 from __future__ import annotations
 
@@ -66,39 +67,91 @@ def kernel_bytes(stats: np.ndarray, nx: int, nu: int, N: int) -> dict:
     }
 
 
-def cpu_baseline(cfg, batch, budget_s: float = 12.0, max_inst: int = 64) -> dict:
-    """Oracle (numpy fp64 restatement) on one core over a bounded sample of
-    the same instances.  Test infrastructure used only as the baseline leg."""
+def _oracle_solve_one(args):
+    """Worker: one oracle solve of instance i (CPU restatement, maxiter=10)."""
+    cfg_kw, i = args
     from oracle import fddp, ocp  # noqa: WPS433 (checker import, baseline leg only)
+
+    batch = _CPU_STATE["batch"]
+    prob = ocp.Problem(batch.x0[i], batch.node_ref[i, :, :3], batch.node_ref[i, :, 3:], batch.inst_ref[i, :14],
+                       batch.inst_ref[i, 14:], bool(batch.surface[i]))
+    s = fddp.SolverBoxFDDP(_CPU_STATE["ocfg"], prob)
+    s.solve(batch.xs_init[i], batch.us_init[i], 10, False)
+    return i
+
+
+_CPU_STATE: dict = {}
+
+
+def _cpu_worker(argv) -> None:
+    """Child process of the cpu_baseline leg (never touches the GPU): rebuilds
+    the same seeded batch, times the oracle over a bounded sample on all the
+    host cores this process may use, prints one JSON object."""
+    import multiprocessing as mp
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int)
+    ap.add_argument("--horizon", type=int)
+    ap.add_argument("--variant")
+    ap.add_argument("--contact")
+    ap.add_argument("--regime")
+    ap.add_argument("--seed", type=int)
+    ap.add_argument("--budget", type=float)
+    a = ap.parse_args(argv)
+    from ffddp import _abi, robot as R, workload
+    from ffddp.config import classical_preset, ff_preset
 
     sys.path.insert(0, str(ROOT / "tests"))
     from helpers import oracle_cfg  # noqa: E402
 
-    ocfg = oracle_cfg(cfg)
+    cfg = ff_preset(a.horizon, a.contact) if a.variant == "ff" else classical_preset(a.horizon, a.contact)
+    ee = R.R_MJ_FROM_PIN @ _abi.frame_placement(R.Q_NEUTRAL)[1]
+    batch = workload.make_batch(a.batch, a.horizon, a.variant, _abi.gravity_torque, ee, seed=a.seed,
+                                regime=a.regime, fk=_abi.frame_placement)
+    _CPU_STATE["batch"] = batch
+    _CPU_STATE["ocfg"] = oracle_cfg(cfg)
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    workers = max(1, min(16, cores))  # the GPU box grants 16 CPUs per GPU
     t0 = time.perf_counter()
-    n = 0
-    for i in range(min(max_inst, batch.B)):
-        prob = ocp.Problem(
-            batch.x0[i], batch.node_ref[i, :, :3], batch.node_ref[i, :, 3:], batch.inst_ref[i, :14],
-            batch.inst_ref[i, 14:], bool(batch.surface[i]),
-        )
-        s = fddp.SolverBoxFDDP(ocfg, prob)
-        s.solve(batch.xs_init[i], batch.us_init[i], 10, False)
-        n += 1
-        if time.perf_counter() - t0 > budget_s and n >= 4:
-            break
+    _oracle_solve_one((None, 0))
+    t1 = time.perf_counter() - t0
+    n = int(min(batch.B, max(workers, workers * max(1, int(a.budget / max(t1, 1e-3))))))
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        pool.map(_oracle_solve_one, [(None, i) for i in range(n)], chunksize=1)
     dt = time.perf_counter() - t0
-    return {
-        "value": n / dt,
-        "unit": "solves/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"first {n} instances of the rank-0 batch (same seed/workload), numpy oracle, maxiter=10, "
-        f"{dt:.1f} s on 1 host thread",
-    }
+    print(json.dumps({
+        "value": n / dt, "unit": "solves/s", "cores": workers, "kind": "port",
+        "sample": f"first {n} instances of the rank-0 batch (same seed/workload), numpy oracle (oracle/fddp.py), "
+                  f"maxiter=10, {workers} worker processes, {dt:.1f} s wall ({t1:.2f} s for one solve on one core)",
+    }))
+
+
+def cpu_baseline(args, seed: int) -> dict:
+    """The oracle timed on the host cores in a child process (the GPU is
+    initialised in this one); bounded to about args.cpu_budget seconds."""
+    import subprocess
+
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--_cpu_worker", "--batch", str(args.batch), "--horizon",
+           str(args.horizon), "--variant", args.variant, "--contact", args.contact, "--regime", args.regime, "--seed",
+           str(seed), "--budget", str(args.cpu_budget)]
+    # one BLAS thread per worker process: the oracle's matrices are tiny and
+    # the workers already cover the cores
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=max(120.0, 10 * args.cpu_budget), env=env)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"value": None, "error": (r.stderr or r.stdout)[-400:]}
+    return json.loads(lines[-1])
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--_cpu_worker":
+        return _cpu_worker(sys.argv[2:])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -237,7 +290,7 @@ def main():
     if rank == 0:
         base = None
         if not args.no_cpu_baseline and world == 1:
-            base = cpu_baseline(cfg, batch, budget_s=args.cpu_budget)
+            base = cpu_baseline(args, shard.shard_seed(1234, rank))
         line = {
             "metric": METRIC,
             "value": value,
