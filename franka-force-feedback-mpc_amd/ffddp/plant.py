@@ -112,6 +112,27 @@ def plant_params(timestep: float = DEFAULT_TIMESTEP, n_substeps: int = 1) -> _ab
     return p
 
 
+def observation_from_record(rec, tau_cmd=None, tilt_deg: float = 0.0) -> Observation:
+    """Observation of one FFDDP_PLANT_OBS record (no torque filters: the
+    tau_meas* fields hold the unfiltered tau_total)."""
+    rec = np.asarray(rec, dtype=float)
+    tau_cmd = np.zeros(7) if tau_cmd is None else np.asarray(tau_cmd, dtype=float).copy()
+    tau_c = rec[21:28].copy()
+    total = tau_cmd + tau_c
+    ncon = int(round(rec[47]))
+    fw = rec[43:46].copy()
+    return Observation(
+        q=rec[0:7].copy(), dq=rec[7:14].copy(), tau_meas=total.copy(), tau_meas_filt=total.copy(),
+        tau_meas_act=tau_cmd.copy(), tau_meas_act_filt=tau_cmd.copy(), tau_cmd=tau_cmd, tau_act=np.zeros(7),
+        tau_constraint=tau_c, tau_total=total, tau_bias=rec[14:21].copy(), f_contact_world=fw,
+        f_contact_normal=abs(float(rec[46])) if ncon else 0.0, f_contact_normal_world_z=max(float(fw[2]), 0.0),
+        f_contact_tangent=0.0, contact_count_ee=ncon, contact_count_table=ncon,
+        table_normal_world=table_plane(tilt_deg)[0], ee_pos=rec[28:31].copy(),
+        ee_quat=mat_to_quat_wxyz(rec[34:43].reshape(3, 3)), J_pos=rec[48:69].reshape(3, 7).copy(), J_rot=None,
+        ee_vel=rec[31:34].copy(),
+    )
+
+
 class BatchedPlant:
     """B plant instances on one device; host-array stepping (one launch per
     control step).  ``obs`` rows follow FFDDP_PLANT_OBS (ffddp_plant.hpp)."""
@@ -214,6 +235,13 @@ class PandaTablePlant:
             raise ValueError(f"torque mode expects (7,), got {u.shape}")
         self._tau_cmd = u
         self._bp.step(u, integrate=True)
+        return self.get_observation(with_ee=True, with_jacobian=True)
+
+    def set_state(self, q, v=None) -> Observation:
+        """Write qpos / qvel and run the forward pass (data.qpos[...] = q; mj_forward)."""
+        self._bp.q[0] = np.asarray(q, float).reshape(7)
+        self._bp.v[0] = 0.0 if v is None else np.asarray(v, float).reshape(7)
+        self._bp.step(self._tau_cmd, integrate=False)
         return self.get_observation(with_ee=True, with_jacobian=True)
 
     def bias_torque(self) -> np.ndarray:
