@@ -1950,6 +1950,8 @@ struct ffddp_handle {
   int nstreams = 3;
   std::vector<hipStream_t> streams;
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
+  std::vector<hipEvent_t> stg;  // start-stagger events (FFDDP_STAGGER)
+  int stagger = 2;  // 0 off, 1 after the previous slice's node stage, 2 after its primal kernel
   bool bw_wave = true;
   int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
   int fw_first0 = 2;  // same for iteration 0 (FFDDP_FW_FIRST0)
@@ -2183,6 +2185,11 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
       h->sev.push_back(e);
     }
+    while ((int)h->stg.size() < S) {
+      hipEvent_t e;
+      HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      h->stg.push_back(e);
+    }
   }
   const int Bs = (B + S - 1) / S;
   struct Slice {
@@ -2219,13 +2226,18 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       const double* irefk = iref + b0 * 21;
       const uint8_t* surfk = surf + b0;
       const long nodes = (long)Bk * (N + 1);
+      // optional start stagger: slice k's first node stage waits for slice
+      // k-1's, so the throughput-bound node stages do not all collide
+      if (it == 0 && k > 0 && h->stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
       {
         ProfScope p(h, ss, KC_NODE);
         hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k, nrefk,
                            irefk, surfk, 0);
+        if (it == 0 && h->stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
         hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, ss,
                            h->dc, d, x0k, nrefk, irefk, surfk, 0);
       }
+      if (it == 0 && h->stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_BACKWARD);
         if (h->bw_wave)
@@ -2367,6 +2379,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
       h->fw_first0 = v < 1 ? 1 : (v > NTRIALS ? NTRIALS : v);
     }
     if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
+    if (const char* sg = std::getenv("FFDDP_STAGGER")) h->stagger = std::atoi(sg);
     const char* f1 = std::getenv("FFDDP_FW_FIRST");
     if (f1) {
       const int v = std::atoi(f1);
@@ -2466,6 +2479,7 @@ void ffddp_destroy(ffddp_handle* h) {
   (void)hipSetDevice(h->device);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->sev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->stg) (void)hipEventDestroy(e);
   for (hipStream_t st : h->streams) (void)hipStreamDestroy(st);
   free_all(h);
   delete h;
