@@ -1945,12 +1945,14 @@ struct ffddp_handle {
   std::string err;
   // sub-batch streams: the batch is split into nstreams slices solved on their
   // own HIP streams, so latency-bound phases of one slice overlap with the
-  // throughput-bound phases of another (FFDDP_STREAMS, default 3: with the
-  // caller's stream that is the 4 hardware queues a process gets)
-  int nstreams = 3;
+  // throughput-bound phases of another (FFDDP_STREAMS, default 4: three
+  // created streams plus the caller's stream, the 4 hardware queues a process
+  // gets; FFDDP_CALLER_SLICE=0 puts every slice on a created stream)
+  int nstreams = 4;
   std::vector<hipStream_t> streams;
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
   std::vector<hipEvent_t> stg;  // start-stagger events (FFDDP_STAGGER)
+  bool caller_slice = true;  // FFDDP_CALLER_SLICE
   int stagger = 2;  // 0 off, 1 after the previous slice's node stage, 2 after its primal kernel
   bool bw_wave = true;
   int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
@@ -2202,11 +2204,14 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
     sl[k].b0 = k * Bs;
     sl[k].B = (B - sl[k].b0) < Bs ? (B - sl[k].b0) : Bs;
     sl[k].d = dev_slice(h->d, sl[k].b0, sl[k].B);
-    sl[k].s = S > 1 ? h->streams[k] : s;
+    // FFDDP_CALLER_SLICE: the last slice runs on the caller's stream (its
+    // hardware queue is otherwise idle during the solve)
+    sl[k].s = (S > 1 && !(h->caller_slice && k == S - 1)) ? h->streams[k] : s;
   }
   if (S > 1) {
     HIPCHK(h, hipEventRecord(h->sev[0], s));
-    for (int k = 0; k < S; ++k) HIPCHK(h, hipStreamWaitEvent(sl[k].s, h->sev[0], 0));
+    for (int k = 0; k < S; ++k)
+      if (sl[k].s != s) HIPCHK(h, hipStreamWaitEvent(sl[k].s, h->sev[0], 0));
   }
   const long nxl = nx, N1 = N + 1;
   for (int k = 0; k < S; ++k) {
@@ -2303,6 +2308,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
   if (hipGetLastError() != hipSuccess) return fail(h, FFDDP_E_DEVICE, "kernel launch failed");
   if (S > 1) {
     for (int k = 0; k < S; ++k) {
+      if (sl[k].s == s) continue;
       HIPCHK(h, hipEventRecord(h->sev[1 + k], sl[k].s));
       HIPCHK(h, hipStreamWaitEvent(s, h->sev[1 + k], 0));
     }
@@ -2380,6 +2386,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     }
     if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
     if (const char* sg = std::getenv("FFDDP_STAGGER")) h->stagger = std::atoi(sg);
+    if (const char* cs = std::getenv("FFDDP_CALLER_SLICE")) h->caller_slice = std::atoi(cs) != 0;
     const char* f1 = std::getenv("FFDDP_FW_FIRST");
     if (f1) {
       const int v = std::atoi(f1);
