@@ -15,8 +15,8 @@
 //   k_forward   line search: one lane per (instance, step length) — the ten
 //               trials of SolverFDDP::solve evaluated concurrently (the first
 //               accepted one is the sequential answer).
-//   k_accept    acceptance test / regularisation / stopping (SolverFDDP::solve).
-//   k_commit    copy the accepted trial into (xs, us).
+//   k_accept_commit  acceptance test / regularisation / stopping
+//               (SolverFDDP::solve) and the copy of the accepted trial into (xs, us).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -1503,6 +1503,19 @@ __global__ __launch_bounds__(FW_BLOCK) void k_forward(const DevConsts* __restric
 // joint-parallel (node_calc_g8), which shortens the dependent chain that
 // bounds this kernel.  Lane i < 7 carries joint i of x (q_i, v_i, FF tau_i).
 // ---------------------------------------------------------------------------
+// SolverFDDP::tryStep acceptance of trial tr for an instance in state s
+__device__ __forceinline__ bool trial_accepted(const DevConsts& C, const Dev& d, const InstState& s, int b, int tr) {
+  if (d.trial_fail[(long)b * NTRIALS + tr]) return false;
+  const double a = C.alphas[tr];
+  const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
+  const double dv = s.is_feasible ? 0.0 : d.trial[((long)b * NTRIALS + tr) * 2 + 1];
+  const double dV = s.cost - cost_try;
+  const double d0 = s.dg + dv, d1 = s.dq - 2.0 * dv;
+  const double dVexp = a * (d0 + 0.5 * a * d1);
+  if (dVexp >= 0) return fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp;
+  return fabs(d0) < C.th_grad || dV > C.th_acceptnegstep * dVexp;  // gap-closing branch
+}
+
 // W: waves/SIMD occupancy target (2 while the batch is throughput-bound, 1 for
 // the latency-bound late iterations, where the register budget also holds the
 // next node's K row: PK = prefetch it one node ahead)
@@ -1524,7 +1537,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_
   if (b >= d.B) return;
   const InstState* st = d.st + b;
   if (st->done) return;
-  if (only_more && !st->fw_more) return;
+  if (only_more) {
+    // second pass of the line search: only instances none of whose first
+    // tr0 trials was accepted (the first pass's results are complete: same stream)
+    const InstState sv = *st;
+    bool any = false;
+    for (int t2 = 0; t2 < tr0 && !any; ++t2) any = trial_accepted(C, d, sv, b, t2);
+    if (any) return;
+  }
 #ifdef FFDDP_PHASE_PROF
   const bool pp_on = (b == 0 && tr == 0);
 #endif
@@ -1671,39 +1691,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_
 // ---------------------------------------------------------------------------
 // acceptance / regularisation / stopping: one lane per instance
 // ---------------------------------------------------------------------------
-// SolverFDDP::tryStep acceptance of trial tr for an instance in state s
-__device__ __forceinline__ bool trial_accepted(const DevConsts& C, const Dev& d, const InstState& s, int b, int tr) {
-  if (d.trial_fail[(long)b * NTRIALS + tr]) return false;
-  const double a = C.alphas[tr];
-  const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
-  const double dv = s.is_feasible ? 0.0 : d.trial[((long)b * NTRIALS + tr) * 2 + 1];
-  const double dV = s.cost - cost_try;
-  const double d0 = s.dg + dv, d1 = s.dq - 2.0 * dv;
-  const double dVexp = a * (d0 + 0.5 * a * d1);
-  if (dVexp >= 0) return fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp;
-  return fabs(d0) < C.th_grad || dV > C.th_acceptnegstep * dVexp;  // gap-closing branch
-}
-
-// two-pass line search: does any of the first ntr trials pass?
-__global__ void k_probe(const DevConsts* __restrict__ Cg, Dev d, int ntr) {
-  const DevConsts& C = *Cg;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= d.B) return;
-  InstState& s = d.st[b];
-  if (s.done) return;
-  bool any = false;
-  for (int tr = 0; tr < ntr && !any; ++tr) any = trial_accepted(C, d, s, b, tr);
-  s.fw_more = any ? 0 : 1;
-}
-
-__global__ void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter) {
-  const DevConsts& C = *Cg;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= d.B) return;
+// SolverFDDP::solve after the line search for instance b: first accepted step
+// length, regularisation update, stopping test.  Returns the accepted trial
+// (-1: none, or the instance is done).
+__device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter) {
   InstState s = d.st[b];
   if (s.done) {
     d.st[b].accepted = -1;
-    return;
+    return -1;
   }
   s.iter = iter;
   int acc = -1;
@@ -1740,23 +1735,28 @@ __global__ void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter) {
     s.ok = 1;
   }
   d.st[b] = s;
+  return acc;
 }
 
-__global__ void k_commit(const DevConsts* __restrict__ Cg, Dev d) {
+// acceptance (lane 0) + setCandidate copy of the accepted trial into (xs, us)
+// by the whole block: one block per instance
+__global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restrict__ Cg, Dev d, int iter) {
   const DevConsts& C = *Cg;
+  const int b = blockIdx.x;
+  if (b >= d.B) return;
+  __shared__ int acc_s;
+  if (threadIdx.x == 0) acc_s = accept_instance(C, d, b, iter);
+  __syncthreads();
+  const int acc = acc_s;
+  if (acc < 0) return;
   const int N = C.N, nx = C.nx;
   const long perX = (long)(N + 1) * nx, perU = (long)N * NU;
-  const long total = (long)d.B * (perX + perU);
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int b = (int)(i / (perX + perU));
-    const long r = i % (perX + perU);
-    const int acc = d.st[b].accepted;
-    if (acc < 0) continue;
-    if (r < perX)
-      d.xs[(long)b * perX + r] = d.xs_try[((long)b * NTRIALS + acc) * perX + r];
-    else
-      d.us[(long)b * perU + (r - perX)] = d.us_try[((long)b * NTRIALS + acc) * perU + (r - perX)];
-  }
+  const double* sx = d.xs_try + ((long)b * NTRIALS + acc) * perX;
+  const double* su = d.us_try + ((long)b * NTRIALS + acc) * perU;
+  double* dx = d.xs + (long)b * perX;
+  double* du = d.us + (long)b * perU;
+  for (long i = threadIdx.x; i < perX; i += blockDim.x) dx[i] = sx[i];
+  for (long i = threadIdx.x; i < perU; i += blockDim.x) du[i] = su[i];
 }
 
 // solution read-back helpers: iter/ok, contact force at knots 0 and 1
@@ -2269,7 +2269,6 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
           };
           fw(0, n1, 0);
           if (n1 < NTRIALS) {
-            hipLaunchKernelGGL(k_probe, dim3((Bk + 255) / 256), dim3(256), 0, ss, h->dc, d, n1);
             fw(n1, NTRIALS - n1, 1);
           }
         } else {
@@ -2279,11 +2278,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       }
       {
         ProfScope p(h, ss, KC_ACCEPT);
-        hipLaunchKernelGGL(k_accept, dim3((Bk + 255) / 256), dim3(256), 0, ss, h->dc, d, it);
-      }
-      {
-        ProfScope p(h, ss, KC_COMMIT);
-        hipLaunchKernelGGL(k_commit, dim3(2048), dim3(256), 0, ss, h->dc, d);
+        hipLaunchKernelGGL(k_accept_commit, dim3(Bk), dim3(64), 0, ss, h->dc, d, it);
       }
     }
   }
