@@ -54,15 +54,24 @@ def algorithmic_words(nx: int, nu: int, N: int):
 
 
 def kernel_bytes(stats: np.ndarray, nx: int, nu: int, N: int) -> dict:
-    """Algorithmic bytes of one solve of the whole batch, per kernel class."""
+    """Algorithmic bytes of one solve of the whole batch, per kernel class
+    (one kernel per class): node = the calcDiff record (A words per running
+    node), primal = the calc's reads (x_t, u_t, x_t+1, refs) and writes (gap,
+    cost), backward = B words per node, forward / forward2 = C words per node
+    for every step length the first / second line-search pass evaluated."""
     w = algorithmic_words(nx, nu, N)
     n_calc = stats[:, 4].astype(np.float64)
     n_bw = stats[:, 0].astype(np.float64)
-    n_trials = stats[:, 1].astype(np.float64)
+    ev1 = stats[:, 6].astype(np.float64)
+    ev2 = stats[:, 7].astype(np.float64)
+    primal_words = 2 * nx + nu + 6 + nx + 1
+    per_trial = N * w["C"] + w["C_T"]
     return {
         "node": 8.0 * float(np.sum(n_calc)) * (N * w["A"] + w["A_T"]),
+        "primal": 8.0 * float(np.sum(n_calc)) * (N + 1) * primal_words,
         "backward": 8.0 * float(np.sum(n_bw)) * (N * w["B"] + w["B_T"]),
-        "forward": 8.0 * float(np.sum(n_trials)) * (N * w["C"] + w["C_T"]),
+        "forward": 8.0 * float(np.sum(ev1)) * per_trial,
+        "forward2": 8.0 * float(np.sum(ev2)) * per_trial,
         "io": 8.0 * stats.shape[0] * w["IO"],
     }
 
@@ -226,7 +235,7 @@ def main():
     dom = None
     if not args.no_profile:
         warm_prof = solver.profile_read(reset=True)
-        dom = max(("node", "backward", "forward"), key=lambda k: warm_prof[k][0])
+        dom = max(("primal", "node", "backward", "forward"), key=lambda k: warm_prof[k][0])
         solver.profile([dom])
         solver.profile_read(reset=True)
     elapsed = shard.timed_steps(step, args.steps, lambda: torch.cuda.synchronize(dev))
@@ -323,6 +332,7 @@ def main():
                 "mean_iter": float(np.mean(iters)),
                 "mean_iters_run": float(np.mean(stats[:, 0])),
                 "mean_trials": float(np.mean(stats[:, 1])),
+                "mean_trials_evaluated": float(np.mean(stats[:, 6] + stats[:, 7])),
                 "cost_finite_frac": float(np.mean(np.isfinite(cost))),
             },
             "kernels": kernels,

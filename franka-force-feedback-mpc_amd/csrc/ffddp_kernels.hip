@@ -61,7 +61,8 @@ struct InstState {
   double preg, cost, dg, dq, stop;
   int is_feasible, was_feasible, done, ok, iter, recalc, accepted, bw_ok;
   int n_iters, n_trials, n_retries, n_backward, n_calc, n_forward;
-  int fw_more;  // two-pass line search: first trials rejected, evaluate the rest
+  int fw_more;  // (unused)
+  int n_eval1, n_eval2;  // line-search trials evaluated by the first / second pass
 };
 
 struct Dev {
@@ -114,6 +115,7 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
       s.accepted = -1;
       s.bw_ok = 0;
       s.n_iters = s.n_trials = s.n_retries = s.n_backward = s.n_calc = s.n_forward = 0;
+      s.n_eval1 = s.n_eval2 = 0;
       s.fw_more = 0;
       d.st[i] = s;
     }
@@ -1694,7 +1696,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_
 // SolverFDDP::solve after the line search for instance b: first accepted step
 // length, regularisation update, stopping test.  Returns the accepted trial
 // (-1: none, or the instance is done).
-__device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter) {
+__device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int n1) {
   InstState s = d.st[b];
   if (s.done) {
     d.st[b].accepted = -1;
@@ -1719,6 +1721,10 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter) {
     }
   }
   if (acc < 0) s.recalc = 0;  // (xs, us) unchanged: node data stays valid
+  // step lengths the line-search kernels evaluated (first pass: n1; second
+  // pass: the rest, only when none of the first n1 was accepted)
+  s.n_eval1 += n1;
+  if (acc < 0 || acc >= n1) s.n_eval2 += NTRIALS - n1;
   s.n_trials += tried;
   s.n_forward += 1;
   s.accepted = acc;
@@ -1740,12 +1746,12 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter) {
 
 // acceptance (lane 0) + setCandidate copy of the accepted trial into (xs, us)
 // by the whole block: one block per instance
-__global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restrict__ Cg, Dev d, int iter) {
+__global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1) {
   const DevConsts& C = *Cg;
   const int b = blockIdx.x;
   if (b >= d.B) return;
   __shared__ int acc_s;
-  if (threadIdx.x == 0) acc_s = accept_instance(C, d, b, iter);
+  if (threadIdx.x == 0) acc_s = accept_instance(C, d, b, iter, n1);
   __syncthreads();
   const int acc = acc_s;
   if (acc < 0) return;
@@ -1783,6 +1789,8 @@ __global__ __launch_bounds__(64) void k_finalize(const DevConsts* __restrict__ C
       stats[(long)b * FFDDP_NSTATS + 3] = s.n_backward;
       stats[(long)b * FFDDP_NSTATS + 4] = s.n_calc;
       stats[(long)b * FFDDP_NSTATS + 5] = s.n_forward;
+      stats[(long)b * FFDDP_NSTATS + 6] = s.n_eval1;
+      stats[(long)b * FFDDP_NSTATS + 7] = s.n_eval2;
     }
   }
   if (fn_pred == nullptr) return;
@@ -2144,7 +2152,9 @@ struct ProfScope {
   }
 };
 
-enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE };
+// profiling classes: one kernel per class (KC_COMMIT is no longer launched:
+// the copy is fused into k_accept_commit)
+enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE, KC_FORWARD2, KC_PRIMAL };
 
 // the per-instance slice [b0, b0 + Bk) of the handle workspace
 Dev dev_slice(const Dev& d0, int b0, int Bk) {
@@ -2235,10 +2245,13 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       // k-1's, so the throughput-bound node stages do not all collide
       if (it == 0 && k > 0 && h->stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
       {
-        ProfScope p(h, ss, KC_NODE);
+        ProfScope p(h, ss, KC_PRIMAL);
         hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k, nrefk,
                            irefk, surfk, 0);
-        if (it == 0 && h->stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
+      }
+      if (it == 0 && h->stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
+      {
+        ProfScope p(h, ss, KC_NODE);
         hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, ss,
                            h->dc, d, x0k, nrefk, irefk, surfk, 0);
       }
@@ -2251,34 +2264,37 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
           hipLaunchKernelGGL((k_backward<FF>), dim3((Bk + (FF ? 1 : 3)) / (FF ? 2 : 4)), dim3(BW_BLOCK), 0, ss, h->dc, d,
                              it);
       }
-      {
-        ProfScope p(h, ss, KC_FORWARD);
-        if (h->fw_group) {
-          // first pass: trials 0..n1-1; iteration 0 of a cold start almost
-          // always accepts alpha = 1 or 1/2 (fw_first0), later ones up to 1/8
-          const int n1 = it == 0 ? h->fw_first0 : h->fw_first;
-          const bool late = it >= h->fw_late_it;
-          auto fw = [&](int tr0, int ntr, int more) {
-            const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
-            if (late)
-              hipLaunchKernelGGL((k_forward_g8<NC, FF, 1, true>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
-                                 surfk, tr0, ntr, more);
-            else
-              hipLaunchKernelGGL((k_forward_g8<NC, FF>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk,
-                                 tr0, ntr, more);
-          };
+      int n1 = NTRIALS;
+      if (h->fw_group) {
+        // first pass: trials 0..n1-1; iteration 0 of a cold start almost
+        // always accepts alpha = 1 or 1/2 (fw_first0), later ones up to 1/8
+        n1 = it == 0 ? h->fw_first0 : h->fw_first;
+        const bool late = it >= h->fw_late_it;
+        auto fw = [&](int tr0, int ntr, int more) {
+          const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
+          if (late)
+            hipLaunchKernelGGL((k_forward_g8<NC, FF, 1, true>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
+                               surfk, tr0, ntr, more);
+          else
+            hipLaunchKernelGGL((k_forward_g8<NC, FF>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk, tr0,
+                               ntr, more);
+        };
+        {
+          ProfScope p(h, ss, KC_FORWARD);
           fw(0, n1, 0);
-          if (n1 < NTRIALS) {
-            fw(n1, NTRIALS - n1, 1);
-          }
-        } else {
-          hipLaunchKernelGGL((k_forward<NC, FF>), dim3((int)(((long)Bk * NTRIALS + FW_BLOCK - 1) / FW_BLOCK)),
-                             dim3(FW_BLOCK), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk);
         }
+        if (n1 < NTRIALS) {
+          ProfScope p(h, ss, KC_FORWARD2);
+          fw(n1, NTRIALS - n1, 1);
+        }
+      } else {
+        ProfScope p(h, ss, KC_FORWARD);
+        hipLaunchKernelGGL((k_forward<NC, FF>), dim3((int)(((long)Bk * NTRIALS + FW_BLOCK - 1) / FW_BLOCK)),
+                           dim3(FW_BLOCK), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk);
       }
       {
         ProfScope p(h, ss, KC_ACCEPT);
-        hipLaunchKernelGGL(k_accept_commit, dim3(Bk), dim3(64), 0, ss, h->dc, d, it);
+        hipLaunchKernelGGL(k_accept_commit, dim3(Bk), dim3(64), 0, ss, h->dc, d, it, n1);
       }
     }
   }

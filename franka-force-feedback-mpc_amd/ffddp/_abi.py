@@ -38,8 +38,8 @@ SYMBOLS = (
     "ffddp_plant_step_dev",
 )
 PLANT_OBS = 69
-NSTATS = 6
-KERNEL_CLASSES = ("init", "node", "backward", "forward", "accept", "commit", "finalize")
+NSTATS = 8
+KERNEL_CLASSES = ("init", "node", "backward", "forward", "accept", "commit", "finalize", "forward2", "primal")
 
 
 class Robot(C.Structure):

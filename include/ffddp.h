@@ -31,8 +31,8 @@ extern "C" {
 #define FFDDP_NQ 7      /* Panda arm joints (fingers locked, crocoddyl_classical.py:189-197) */
 #define FFDDP_NU 7      /* ActuationModelFull: nu = nv (:147) */
 #define FFDDP_MAX_NC 3  /* ContactModel1D (nc=1) or ContactModel3D (nc=3) */
-#define FFDDP_NSTATS 6  /* per-instance counters returned by the solve */
-#define FFDDP_NKERNELS 7 /* kernel classes reported by ffddp_profile_read */
+#define FFDDP_NSTATS 8  /* per-instance counters returned by the solve */
+#define FFDDP_NKERNELS 9 /* kernel classes reported by ffddp_profile_read */
 
 enum {
   FFDDP_OK = 0,
@@ -135,8 +135,10 @@ const char* ffddp_last_error(const ffddp_handle* h);
  *                    [1] line-search trials a sequential solver executes,
  *                    [2] regularisation retries of the backward pass,
  *                    [3] backward passes run, [4] calcDiff evaluations,
- *                    [5] forward (line-search) launches — for the roofline
- *                    byte count. */
+ *                    [5] forward (line-search) launches,
+ *                    [6] / [7] step lengths evaluated by the first / second
+ *                    line-search pass — for the roofline byte count
+ *                    (SURVEY.md §8(d)). */
 int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* node_ref,
                       const double* inst_ref, const uint8_t* surface, const double* xs_init,
                       const double* us_init, int maxiter, int is_feasible, double* xs, double* us,
@@ -169,14 +171,16 @@ int ffddp_frame_placement(const ffddp_robot* robot, const double* q, double* R, 
 int ffddp_gravity_torque(const ffddp_robot* robot, int B, const double* q, double* tau);
 
 /* Optional per-kernel device timing (HIP events recorded around every launch
- * on the launch stream).  Kernel classes, in order: init, node (calc+calcDiff),
- * backward, forward (line search), accept, commit, finalize.
+ * on the launch stream), one kernel per class.  Classes, in order: init,
+ * node (calcDiff tangents + Gauss-Newton), backward, forward (line search,
+ * first pass), accept (acceptance + copy of the accepted trial), commit
+ * (unused), finalize, forward2 (line search, second pass), primal (calc).
  * `classes` is a bit mask over those classes (bit i = class i; 0 = off,
  * FFDDP_PROFILE_ALL = every class).  Timing only the kernel of interest keeps
  * the event overhead out of the other launches.
  * ffddp_profile_read synchronises the recorded events and returns, per class,
  * the summed milliseconds and launch counts since the last reset. */
-#define FFDDP_PROFILE_ALL 0x7F
+#define FFDDP_PROFILE_ALL 0x1FF
 int ffddp_profile_enable(ffddp_handle* h, int classes);
 int ffddp_profile_read(ffddp_handle* h, double* ms, int64_t* launches, int reset);
 

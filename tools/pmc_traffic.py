@@ -4,7 +4,7 @@ bytes for the solver kernels (MI355X_MICROARCH.md §HBM: FETCH_SIZE is reported
 in KiB and counts half the bytes of wide streaming reads on gfx950, so it is
 doubled; WRITE_SIZE is taken as is).
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG SOLVES OUT_JSON
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG SOLVES OUT_JSON [SLICE_B]
   CONFIG is bench.py's "<variant>/<contact>/B<B>/N<N>" key; SOLVES the number
   of batched solves each profiled run executed (warmup + steps).  Bytes are
   reported per solve per kernel class (bench.py divides by its own launch
@@ -18,17 +18,19 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-# kernel name -> bench/profiler class (ffddp_profile_read classes)
+# kernel name -> bench/profiler class (ffddp_profile_read classes, one kernel each)
 CLASS_OF = (
-    ("k_primal", "node"), ("k_node", "node"), ("k_backward", "backward"), ("k_forward", "forward"),
-    ("k_probe", "forward"), ("k_accept", "accept"), ("k_commit", "commit"), ("k_init", "init"),
-    ("k_finalize", "finalize"),
+    ("k_primal", "primal"), ("k_node", "node"), ("k_backward", "backward"), ("k_forward", "forward"),
+    ("k_accept", "accept"), ("k_init", "init"), ("k_finalize", "finalize"),
 )
+SLICE_B = 1024  # instances per sub-batch slice (B / FFDDP_STREAMS)
 
 
-def kclass(name: str):
+def kclass(name: str, grid: int = 0):
     for key, c in CLASS_OF:
         if key in name:
+            if c == "forward" and grid > 5 * 8 * SLICE_B:
+                return "forward2"  # second pass: >= 6 step lengths x 8 lanes per instance
             return c
     return None
 
@@ -46,7 +48,7 @@ def read_counter(d: Path, counter: str):
                 low = {k.lower(): v for k, v in row.items()}
                 if low.get("counter_name") != counter:
                     continue
-                c = kclass(low.get("kernel_name", ""))
+                c = kclass(low.get("kernel_name", ""), int(float(low.get("grid_size", 0) or 0)))
                 if c is None:
                     continue
                 tot[c] += float(low["counter_value"])
@@ -55,7 +57,10 @@ def read_counter(d: Path, counter: str):
 
 
 def main():
+    global SLICE_B
     fetch_dir, write_dir, config, solves, out = sys.argv[1:6]
+    if len(sys.argv) > 6:
+        SLICE_B = int(sys.argv[6])
     solves = float(solves)
     fe = read_counter(Path(fetch_dir), "FETCH_SIZE")
     wr = read_counter(Path(write_dir), "WRITE_SIZE")
