@@ -1,0 +1,105 @@
+"""GPU: batch-size independence and the solve's edge cases, through the C-ABI.
+
+* At the BASELINE size (B = 4096, 4 slices on 4 streams, staggered) and at an
+  uneven size (B = 517), every instance's solution equals, BIT FOR BIT, the
+  solution of the same instance solved in a small batch on one stream: the
+  per-instance arithmetic does not depend on batch composition, slicing or
+  stream overlap (a size-independent property at full size).  A spread of
+  those instances is also checked against the oracle.
+* is_feasible = True with a feasible warm start (the previous solution),
+  maxiter = 0, B = 0, and B above max_batch.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from ffddp import BatchedBoxFDDP, FfddpError
+
+from helpers import make_batch, oracle_cfg, oracle_problem, oracle_solve, product_cfg, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _sub(batch, idx):
+    import copy
+
+    b = copy.copy(batch)
+    for f in ("x0", "node_ref", "inst_ref", "surface", "xs_init", "us_init", "t0"):
+        setattr(b, f, np.ascontiguousarray(getattr(batch, f)[idx]))
+    return b
+
+
+@pytest.mark.parametrize("B", [4096, 517])
+def test_full_batch_equals_small_batches(B, monkeypatch):
+    N = 30
+    cfg = product_cfg("classical", N)
+    batch = make_batch("classical", B, N, seed=77)
+    big = BatchedBoxFDDP(cfg, max_batch=B)
+    big.solve(batch, maxiter=10)
+    # one-stream reference solver for small batches
+    monkeypatch.setenv("FFDDP_STREAMS", "1")
+    small = BatchedBoxFDDP(cfg, max_batch=8)
+    rng = np.random.default_rng(1)
+    picks = np.unique(np.concatenate([[0, 1, B // 4 - 1, B // 4, B // 2, B - 1], rng.integers(0, B, 10)]))
+    for i0 in range(0, len(picks), 8):
+        idx = picks[i0:i0 + 8]
+        small.solve(_sub(batch, idx), maxiter=10)
+        for j, i in enumerate(idx):
+            for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred"):
+                a, b = getattr(big, name)[i], getattr(small, name)[j]
+                assert np.array_equal(a, b, equal_nan=True), (name, int(i))
+    # a spread of them against the oracle
+    for i in picks[::4]:
+        ok_o, s = oracle_solve(cfg, batch, int(i))
+        assert bool(big.ok[i]) == bool(ok_o) and int(big.iter[i]) == int(s.iter)
+        assert rel_err(big.xs[i], s.xs) < 1e-6 and rel_err(big.us[i], s.us) < 1e-6
+        assert rel_err(big.cost[i], s.cost) < 1e-6
+    assert np.all(np.isfinite(big.cost)) and np.mean(big.ok) > 0.9
+    big.close()
+    small.close()
+
+
+def test_feasible_warm_start_matches_oracle():
+    from oracle import fddp
+
+    N, B = 20, 4
+    cfg = product_cfg("classical", N)
+    batch = make_batch("classical", B, N, seed=91, surface=1)
+    s1 = BatchedBoxFDDP(cfg, max_batch=B)
+    s1.solve(batch, maxiter=10)
+    xs0, us0 = s1.xs.copy(), s1.us.copy()
+    # a dynamically feasible guess: the converged solution (gaps closed)
+    ok = s1.solve(batch, maxiter=3, is_feasible=True, xs_init=xs0, us_init=us0)
+    for i in range(B):
+        so = fddp.SolverBoxFDDP(oracle_cfg(cfg), oracle_problem(batch, i, N))
+        ok_o = so.solve(xs0[i], us0[i], 3, True)
+        assert bool(ok[i]) == bool(ok_o) and int(s1.iter[i]) == int(so.iter)
+        assert rel_err(s1.xs[i], so.xs) < 1e-6 and rel_err(s1.us[i], so.us) < 1e-6
+        assert rel_err(s1.cost[i], so.cost) < 1e-6
+    s1.close()
+
+
+def test_maxiter_zero_and_sizes():
+    from oracle import fddp
+
+    N, B = 10, 3
+    cfg = product_cfg("classical", N)
+    batch = make_batch("classical", B, N, seed=5)
+    s = BatchedBoxFDDP(cfg, max_batch=B)
+    ok = s.solve(batch, maxiter=0)
+    for i in range(B):
+        so = fddp.SolverBoxFDDP(oracle_cfg(cfg), oracle_problem(batch, i, N))
+        ok_o = so.solve(batch.xs_init[i], batch.us_init[i], 0, False)
+        assert bool(ok[i]) == bool(ok_o)
+        np.testing.assert_array_equal(s.xs[i], batch.xs_init[i])
+        np.testing.assert_array_equal(s.us[i], batch.us_init[i])
+    with pytest.raises(FfddpError):
+        s.solve(make_batch("classical", B + 1, N, seed=6))
+    empty = make_batch("classical", 1, N, seed=6)
+    for f in ("x0", "node_ref", "inst_ref", "surface", "xs_init", "us_init", "t0"):
+        setattr(empty, f, getattr(empty, f)[:0])
+    assert s.solve(empty).shape == (0,)
+    s.close()
