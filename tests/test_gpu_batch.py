@@ -6,7 +6,7 @@
   per-instance arithmetic does not depend on batch composition, slicing or
   stream overlap (a size-independent property at full size).  A spread of
   those instances is also checked against the oracle.
-* is_feasible = True with a feasible warm start (the previous solution),
+* is_feasible = True with a feasible warm start (rollout of the cold controls),
   maxiter = 0, B = 0, and B above max_batch.
 """
 from __future__ import annotations
@@ -63,19 +63,28 @@ def test_full_batch_equals_small_batches(B, monkeypatch):
 
 
 def test_feasible_warm_start_matches_oracle():
-    from oracle import fddp
+    """is_feasible = True: xs_init is the rollout of us_init (gravity torques)
+    through the dynamics, so the guess has no gaps (SolverFDDP feasible start)."""
+    from oracle import fddp, ocp
 
     N, B = 20, 4
     cfg = product_cfg("classical", N)
     batch = make_batch("classical", B, N, seed=91, surface=1)
-    s1 = BatchedBoxFDDP(cfg, max_batch=B)
-    s1.solve(batch, maxiter=10)
-    xs0, us0 = s1.xs.copy(), s1.us.copy()
-    # a dynamically feasible guess: the converged solution (gaps closed)
-    ok = s1.solve(batch, maxiter=3, is_feasible=True, xs_init=xs0, us_init=us0)
+    ocfg = oracle_cfg(cfg)
+    xs0 = np.zeros((B, N + 1, 14))
     for i in range(B):
-        so = fddp.SolverBoxFDDP(oracle_cfg(cfg), oracle_problem(batch, i, N))
-        ok_o = so.solve(xs0[i], us0[i], 3, True)
+        prob = oracle_problem(batch, i, N)
+        x = batch.x0[i].copy()
+        xs0[i, 0] = x
+        for t in range(N):
+            x = ocp.running_eval(ocfg, prob, t, x, batch.us_init[i, t], False)["xnext"]
+            xs0[i, t + 1] = x
+    us0 = batch.us_init.copy()
+    s1 = BatchedBoxFDDP(cfg, max_batch=B)
+    ok = s1.solve(batch, maxiter=4, is_feasible=True, xs_init=xs0, us_init=us0)
+    for i in range(B):
+        so = fddp.SolverBoxFDDP(ocfg, oracle_problem(batch, i, N))
+        ok_o = so.solve(xs0[i], us0[i], 4, True)
         assert bool(ok[i]) == bool(ok_o) and int(s1.iter[i]) == int(so.iter)
         assert rel_err(s1.xs[i], so.xs) < 1e-6 and rel_err(s1.us[i], so.us) < 1e-6
         assert rel_err(s1.cost[i], so.cost) < 1e-6
