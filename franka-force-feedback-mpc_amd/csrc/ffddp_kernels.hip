@@ -29,6 +29,7 @@
 
 #include "ffddp_group.hpp"
 #include "ffddp_plant.hpp"
+#include "ffddp_primal_g8.hpp"
 
 using namespace ffddp;
 
@@ -49,6 +50,9 @@ constexpr int FW_BLOCK = 64;
 #endif
 #ifndef PRIMAL_WAVES
 #define PRIMAL_WAVES 1
+#endif
+#ifndef PRIMAL_G8_WAVES
+#define PRIMAL_G8_WAVES 2
 #endif
 #ifndef QC_UNROLL
 #define QC_UNROLL 1
@@ -212,6 +216,88 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_WAVES
   if (t == 0) {
     double* f = d.fs + (long)b * (N + 1) * nx;
     for (int i = 0; i < nx; ++i) f[i] = feas ? 0.0 : x0[(long)b * nx + i] - y[i];
+  }
+}
+
+// k_primal on 8-lane groups (ffddp_primal_g8.hpp): one group per node, the
+// rigid-body recursions as log-depth scans; same outputs as k_primal.
+template <int NC, bool FF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_G8_WAVES))) void k_primal_g8(
+    const DevConsts* __restrict__ Cg, Dev d, const double* __restrict__ x0, const double* __restrict__ node_ref,
+    const double* __restrict__ inst_ref, const uint8_t* __restrict__ surface, int force_all) {
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  constexpr int nx = FF ? 21 : 14;
+  const long node = (blockIdx.x * (long)blockDim.x + threadIdx.x) / G8;
+  const int li = g8_lane();
+  const bool J = li < NQ;
+  const int ji = J ? li : 0;
+  const int b = (int)(node / (N + 1)), t = (int)(node % (N + 1));
+  if (b >= d.B) return;
+  if (!force_all && (d.st[b].done != 0 || d.st[b].recalc == 0)) return;
+  const bool surf = surface[b] != 0;
+  const bool terminal = t == N;
+  const int mode = !terminal ? MODE_RUNNING : (FF ? MODE_TERMINAL_U : MODE_TERMINAL_X);
+  const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
+  const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
+  const double* xreg = inst_ref + (long)b * 21;
+  const double* uin = FF ? (y + 14) : (terminal ? nullptr : d.us + ((long)b * N + t) * NU);
+  const double q = y[ji], v = y[7 + ji];
+  const double u = (uin != nullptr) ? uin[ji] : 0.0;
+  double lam[3];
+  const double pc = node_primal_g8<NC>(C, mode, surf, q, v, u, xreg[ji], xreg[7 + ji], xreg[14 + ji], ref,
+                                       d.prim + node, d.link + node * LK_ALLOC, lam);
+  double* rec = d.rec_buf + node * d.rec;
+  // node cost (IAM scaling, FF augmentation terms): per-lane shares summed over the group
+  double c = FF ? C.dt * pc : (terminal ? pc : C.dt * pc);
+  if (FF) {
+    double part = 0.0;
+    if (J) {
+      if (C.w_y > 0.0) {
+        double a_ = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const double dd = y[7 * k + li] - x0[(long)b * nx + 7 * k + li];
+          a_ += C.Wy2[7 * k + li] * dd * dd;
+        }
+        part += 0.5 * C.w_y * a_;
+      }
+      if (!terminal) {
+        const double ww = d.us[((long)b * N + t) * NU + li];
+        if (C.w_w > 0.0) part += 0.5 * C.w_w * (ww * ww);
+        if (C.w_ws > 0.0) {
+          const double ov = fabs(ww) - C.ws_lim[li];
+          const double o = ov > 0.0 ? ov : 0.0;
+          part += C.w_ws * (0.5 * (o * o));
+        }
+      }
+    }
+    c += g8_sum(part);
+  }
+  if (li == 0) {
+    rec[rec_off_cost(nx)] = c;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) rec[rec_off_lam(nx) + r] = (mode == MODE_TERMINAL_X) ? 0.0 : lam[r];
+  }
+  // gaps fs[t+1] = xnext_t - xs[t+1] ; fs[0] = x0 - xs[0]  (zero once feasible)
+  const bool feas = d.st[b].is_feasible != 0;
+  if (J) {
+    if (!terminal) {
+      double* f = d.fs + ((long)b * (N + 1) + t + 1) * nx;
+      const double* yn = d.xs + ((long)b * (N + 1) + t + 1) * nx;
+      const double dt = C.dt;
+      const double a = d.prim[node].a[li];  // this lane's own store
+      const double qn = (mode == MODE_TERMINAL_X) ? q : q + (v * dt + a * dt * dt);
+      const double vn = (mode == MODE_TERMINAL_X) ? v : v + a * dt;
+      f[li] = feas ? 0.0 : qn - yn[li];
+      f[7 + li] = feas ? 0.0 : vn - yn[7 + li];
+      if (FF) f[14 + li] = feas ? 0.0 : (C.alpha * y[14 + li] + C.beta * d.us[((long)b * N + t) * NU + li]) - yn[14 + li];
+    }
+    if (t == 0) {
+      double* f = d.fs + (long)b * (N + 1) * nx;
+#pragma unroll
+      for (int k = 0; k < (FF ? 3 : 2); ++k) f[7 * k + li] = feas ? 0.0 : x0[(long)b * nx + 7 * k + li] - y[7 * k + li];
+    }
   }
 }
 
@@ -1961,6 +2047,7 @@ struct ffddp_handle {
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
   std::vector<hipEvent_t> stg;  // start-stagger events (FFDDP_STAGGER)
   bool caller_slice = true;  // FFDDP_CALLER_SLICE
+  bool primal_g8 = true;  // calc on 8-lane groups (FFDDP_PRIMAL=lane: one lane per node)
   int stagger = 2;  // 0 off, 1 after the previous slice's node stage, 2 after its primal kernel
   bool bw_wave = true;
   int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
@@ -2246,8 +2333,12 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       if (it == 0 && k > 0 && h->stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
       {
         ProfScope p(h, ss, KC_PRIMAL);
-        hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k, nrefk,
-                           irefk, surfk, 0);
+        if (h->primal_g8)
+          hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k,
+                             nrefk, irefk, surfk, 0);
+        else
+          hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k, nrefk,
+                             irefk, surfk, 0);
       }
       if (it == 0 && h->stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
@@ -2343,8 +2434,12 @@ int launch_solve(ffddp_handle* h, int B, const double* x0, const double* nref, c
 template <int NC, bool FF>
 void launch_node(ffddp_handle* h, Dev d, int B, hipStream_t s, int force_all) {
   const long nodes = (long)B * (h->hc.N + 1);
-  hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
-                     h->in_nref, h->in_iref, h->in_surf, force_all);
+  if (h->primal_g8)
+    hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
+                       h->in_nref, h->in_iref, h->in_surf, force_all);
+  else
+    hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
+                       h->in_nref, h->in_iref, h->in_surf, force_all);
   hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, s, h->dc,
                      d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all);
 }
@@ -2398,6 +2493,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
     if (const char* sg = std::getenv("FFDDP_STAGGER")) h->stagger = std::atoi(sg);
     if (const char* cs = std::getenv("FFDDP_CALLER_SLICE")) h->caller_slice = std::atoi(cs) != 0;
+    if (const char* pg = std::getenv("FFDDP_PRIMAL")) h->primal_g8 = std::strcmp(pg, "lane") != 0;
     const char* f1 = std::getenv("FFDDP_FW_FIRST");
     if (f1) {
       const int v = std::atoi(f1);
