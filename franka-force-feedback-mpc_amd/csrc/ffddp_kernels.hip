@@ -2051,7 +2051,12 @@ struct ffddp_handle {
   int stagger = 2;  // 0 off, 1 after the previous slice's node stage, 2 after its primal kernel
   bool bw_wave = true;
   int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
-  int fw_first0 = 2;  // same for iteration 0 (FFDDP_FW_FIRST0)
+  // first-pass trial counts of the first iterations (FFDDP_FW_SCHED="2,2,2,2"):
+  // while every instance is active the line search is throughput-bound, so a
+  // 2-trial first pass (alpha 1, 1/2 cover ~90 % of the instances) halves its
+  // work and the second pass, needed there anyway, covers the rest; once most
+  // instances are done the pass is latency-bound and 4 trials in one pass win
+  std::vector<int> fw_sched{2, 2, 2, 2};
   int fw_late_it = 0;  // first iteration using the 1-wave/SIMD line-search variant (FFDDP_FW_LATE_IT)
   bool fw_group = true;  // 8-lane joint-parallel line search; FFDDP_FW=lane selects one lane per trial  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
   // optional per-kernel timing
@@ -2357,9 +2362,10 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       }
       int n1 = NTRIALS;
       if (h->fw_group) {
-        // first pass: trials 0..n1-1; iteration 0 of a cold start almost
-        // always accepts alpha = 1 or 1/2 (fw_first0), later ones up to 1/8
-        n1 = it == 0 ? h->fw_first0 : h->fw_first;
+        // first pass: trials 0..n1-1, per-iteration schedule (fw_sched) then
+        // fw_first; the second pass evaluates the rest for the instances that
+        // accepted none of them
+        n1 = it < (int)h->fw_sched.size() ? h->fw_sched[it] : h->fw_first;
         const bool late = it >= h->fw_late_it;
         auto fw = [&](int tr0, int ntr, int more) {
           const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
@@ -2486,11 +2492,16 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     }
     const char* fw = std::getenv("FFDDP_FW");
     h->fw_group = !(fw && std::strcmp(fw, "lane") == 0);
-    if (const char* f0 = std::getenv("FFDDP_FW_FIRST0")) {
-      const int v = std::atoi(f0);
-      h->fw_first0 = v < 1 ? 1 : (v > NTRIALS ? NTRIALS : v);
-    }
     if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
+    if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
+      h->fw_sched.clear();
+      for (const char* p = fsch; *p;) {
+        const int v = std::atoi(p);
+        h->fw_sched.push_back(v < 1 ? 1 : (v > NTRIALS ? NTRIALS : v));
+        while (*p && *p != ',') ++p;
+        if (*p == ',') ++p;
+      }
+    }
     if (const char* sg = std::getenv("FFDDP_STAGGER")) h->stagger = std::atoi(sg);
     if (const char* cs = std::getenv("FFDDP_CALLER_SLICE")) h->caller_slice = std::atoi(cs) != 0;
     if (const char* pg = std::getenv("FFDDP_PRIMAL")) h->primal_g8 = std::strcmp(pg, "lane") != 0;
