@@ -129,11 +129,21 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
 // ---------------------------------------------------------------------------
 // calc + calcDiff of all nodes
 // ---------------------------------------------------------------------------
+// Per 16-lane group.  The link record is dead once the tangents are in
+// registers, so the residual-Jacobian columns reuse its space (a barrier
+// separates the last read of lk from the first write of col): 18.3 KB per
+// 64-lane block instead of 25 KB, i.e. 8 blocks per CU (the VGPR limit)
+// instead of 6 (the LDS limit).
+struct NodeGroupShared {
+  Primal P;
+  union {
+    double lk[LK_ALLOC];
+    double col[14][NDENSE_MAX];  // residual-Jacobian columns, state directions
+  };
+  double colu[7][FFDDP_MAX_NC];  // force rows, inner-control directions
+};
 struct NodeShared {
-  Primal P[NODE_GPB];
-  double lk[NODE_GPB][LK_ALLOC];
-  double col[NODE_GPB][14][NDENSE_MAX];  // residual-Jacobian columns, state directions
-  double colu[NODE_GPB][7][FFDDP_MAX_NC];  // force rows, inner-control directions
+  NodeGroupShared g[NODE_GPB];
 };
 
 // calc of every node, one lane per node: the primal of calcDiff (dynamics,
@@ -324,14 +334,15 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
   const int mode = !terminal ? MODE_RUNNING : (ff ? MODE_TERMINAL_U : MODE_TERMINAL_X);
   const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
   const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
-  Primal& P = S.P[grp];
+  NodeGroupShared& G = S.g[grp];
+  Primal& P = G.P;
   if (active) {
     const double* src = reinterpret_cast<const double*>(d.prim + node);
     double* dst = reinterpret_cast<double*>(&P);
     constexpr int nw = sizeof(Primal) / sizeof(double);
     for (int e = lane; e < nw; e += NODE_GROUP) dst[e] = src[e];
     const double* ls = d.link + node * LK_ALLOC;
-    for (int e = lane; e < LK_WORDS; e += NODE_GROUP) S.lk[grp][e] = ls[e];
+    for (int e = lane; e < LK_WORDS; e += NODE_GROUP) G.lk[e] = ls[e];
   }
   __syncthreads();
   const bool need_u = mode != MODE_TERMINAL_X;
@@ -341,14 +352,15 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
 #ifdef FFDDP_DUAL_TANGENT
     node_tangent_state<NC>(C, mode, surf, y, ref, P, lane, da, dlam, col);
 #else
-    node_tangent_state_an<NC>(C, mode, surf, S.lk[grp], P, lane, da, dlam, col);
+    node_tangent_state_an<NC>(C, mode, surf, G.lk, P, lane, da, dlam, col);
 #endif
-    for (int r = 0; r < 12 + nc; ++r) S.col[grp][lane][r] = col[r];
   }
-  if (active && lane < 7 && need_u) {
-    node_tangent_control<NC>(C, surf, P, lane, dau, dlamu);
-    for (int r = 0; r < nc; ++r) S.colu[grp][lane][r] = (surf ? dlamu[r] : 0.0);
-  }
+  if (active && lane < 7 && need_u) node_tangent_control<NC>(C, surf, P, lane, dau, dlamu);
+  __syncthreads();  // every lane's reads of lk are done before col overwrites it
+  if (active && lane < 14)
+    for (int r = 0; r < 12 + nc; ++r) G.col[lane][r] = col[r];
+  if (active && lane < 7 && need_u)
+    for (int r = 0; r < nc; ++r) G.colu[lane][r] = (surf ? dlamu[r] : 0.0);
   __syncthreads();
   if (active) {
     double* rec = d.rec_buf + ((long)b * (N + 1) + t) * d.rec;
@@ -366,7 +378,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
       double* Lxx = rec + rec_off_Lxx(nx);
       for (int i = 0; i < 14; ++i) {
         double acc = 0.0;
-        for (int r = 0; r < nd; ++r) acc += S.col[grp][i][r] * D[r] * col[r];
+        for (int r = 0; r < nd; ++r) acc += G.col[i][r] * D[r] * col[r];
         if (i == j) acc += P.Dx[j];
         acc *= sc;
         if (ff && i == j) acc += C.w_y * C.Wy2[j];
@@ -382,7 +394,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
       if (need_u) {
         for (int kk = 0; kk < NU; ++kk) {
           double acc = 0.0;
-          for (int r = 0; r < nc; ++r) acc += col[12 + r] * D[12 + r] * S.colu[grp][kk][r];
+          for (int r = 0; r < nc; ++r) acc += col[12 + r] * D[12 + r] * G.colu[kk][r];
           acc *= sc;
           if (ff)
             Lxx[(14 + kk) * nx + j] = acc;
@@ -398,12 +410,12 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
       double luu[7];
       for (int m = 0; m < NU; ++m) {
         double acc = 0.0;
-        for (int r = 0; r < nc; ++r) acc += S.colu[grp][m][r] * D[12 + r] * S.colu[grp][kk][r];
+        for (int r = 0; r < nc; ++r) acc += G.colu[m][r] * D[12 + r] * G.colu[kk][r];
         if (m == kk) acc += P.Du[kk];
         luu[m] = acc * sc;
       }
       double lu = 0.0;
-      for (int r = 0; r < nc; ++r) lu += S.colu[grp][kk][r] * g[12 + r];
+      for (int r = 0; r < nc; ++r) lu += G.colu[kk][r] * g[12 + r];
       lu = (lu + P.gu[kk]) * sc;
       if (!ff) {
         for (int m = 0; m < NU; ++m) rec[rec_off_Luu(nx) + m * NU + kk] = luu[m];
@@ -413,7 +425,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
         // Lxx_aug column 14+kk: rows 0..13 = Lxu_in[:, kk], rows 14..20 = Luu_in[:, kk] + w_y Wy2
         for (int i = 0; i < 14; ++i) {
           double acc = 0.0;
-          for (int r = 0; r < nc; ++r) acc += S.col[grp][i][12 + r] * D[12 + r] * S.colu[grp][kk][r];
+          for (int r = 0; r < nc; ++r) acc += G.col[i][12 + r] * D[12 + r] * G.colu[kk][r];
           Lxx[i * nx + 14 + kk] = acc * sc;
         }
         for (int m = 0; m < NU; ++m)
