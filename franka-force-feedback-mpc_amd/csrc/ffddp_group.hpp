@@ -493,6 +493,7 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
     if (mode != MODE_TERMINAL_X)
 #pragma unroll
       for (int r = 0; r < NC; ++r) lm[r] = lam[r];
+    if (NC == 3 && C.has_fc) cf += friction_cone(C, lm, nullptr, nullptr, nullptr);
     if (C.has_uni) {
 #pragma unroll
       for (int r = 0; r < NC; ++r) {

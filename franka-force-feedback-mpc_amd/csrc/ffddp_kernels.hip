@@ -6,19 +6,22 @@
 // iteration; all per-instance control flow (regularisation, line-search
 // acceptance, feasibility, stopping) lives on the device, masked per instance:
 //
-//   k_node      calc + calcDiff of every (instance, node):  16-lane group per
-//               node, lane j carries forward-mode direction j (Jacobian column
-//               j), Gauss-Newton Hessians assembled across the group in LDS.
-//   k_backward  Riccati backward pass, one wavefront per instance, blocks in
+//   k_primal_g8 calc of every (instance, node) on an 8-lane group (joint
+//               lanes + EE lane, log-depth scans): dynamics, costs, gaps.
+//   k_node      calcDiff of every (instance, node): 16-lane group per node,
+//               lane j computes state direction j in closed form (Jacobian
+//               column j), Gauss-Newton Hessians assembled across the group in LDS.
+//   k_backward_w  Riccati backward pass, one wavefront per instance, blocks in
 //               LDS; Cholesky (infeasible iterations) or BoxQP gains;
 //               regularisation retries inside the kernel.
-//   k_forward   line search: one lane per (instance, step length) — the ten
-//               trials of SolverFDDP::solve evaluated concurrently (the first
-//               accepted one is the sequential answer).
+//   k_forward_g8  line search: one 8-lane group per (instance, step length) —
+//               the trials of SolverFDDP::solve evaluated concurrently (the
+//               first accepted one is the sequential answer).
 //   k_accept_commit  acceptance test / regularisation / stopping
 //               (SolverFDDP::solve) and the copy of the accepted trial into (xs, us).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,16 +43,11 @@ constexpr int NODE_GROUP = 16;
 #define NODE_BLOCK 64
 #endif
 constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
-constexpr int BW_BLOCK = 64;
-constexpr int FW_BLOCK = 64;
 #ifndef NODE_WAVES
 #define NODE_WAVES 2
 #endif
 #ifndef FW_WAVES
 #define FW_WAVES 2
-#endif
-#ifndef PRIMAL_WAVES
-#define PRIMAL_WAVES 1
 #endif
 #ifndef PRIMAL_G8_WAVES
 #define PRIMAL_G8_WAVES 2
@@ -146,89 +144,6 @@ struct NodeShared {
   NodeGroupShared g[NODE_GPB];
 };
 
-// calc of every node, one lane per node: the primal of calcDiff (dynamics,
-// residuals, activations, cost) plus the node cost, contact force and gap.
-template <int NC, bool FF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_WAVES))) void k_primal(const DevConsts* __restrict__ Cg, Dev d,
-                                               const double* __restrict__ x0,
-                                               const double* __restrict__ node_ref,
-                                               const double* __restrict__ inst_ref,
-                                               const uint8_t* __restrict__ surface, int force_all) {
-  const DevConsts& C = *Cg;
-  const int N = C.N;
-  constexpr int nx = FF ? 21 : 14;
-  const long node = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const int b = (int)(node / (N + 1)), t = (int)(node % (N + 1));
-  if (b >= d.B) return;
-  if (!force_all && (d.st[b].done != 0 || d.st[b].recalc == 0)) return;
-  const bool surf = surface[b] != 0;
-  const bool terminal = t == N;
-  const int mode = !terminal ? MODE_RUNNING : (FF ? MODE_TERMINAL_U : MODE_TERMINAL_X);
-  const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
-  const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
-  const double* xreg = inst_ref + (long)b * 21;
-  const double* uin = FF ? (y + 14) : (terminal ? nullptr : d.us + ((long)b * N + t) * NU);
-  Primal P;
-  node_primal<NC>(C, mode, surf, y, uin, ref, xreg, xreg + 14, P, d.prim + node);
-  {
-    double acc[NQ];
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) acc[i] = (mode == MODE_TERMINAL_X) ? 0.0 : P.a[i];
-    rb_links(C.rb, y, y + NQ, acc, d.link + node * LK_ALLOC);
-  }
-  double* rec = d.rec_buf + node * d.rec;
-  // node cost (IAM scaling, FF augmentation terms)
-  double cost;
-  if (!FF) {
-    cost = terminal ? P.cost : C.dt * P.cost;
-  } else {
-    const double* ww = terminal ? nullptr : d.us + ((long)b * N + t) * NU;
-    double c = C.dt * P.cost;
-    if (C.w_y > 0.0) {
-      double a = 0.0;
-      for (int i = 0; i < 21; ++i) {
-        const double dd = y[i] - x0[(long)b * nx + i];
-        a += C.Wy2[i] * dd * dd;
-      }
-      c += 0.5 * C.w_y * a;
-    }
-    if (!terminal) {
-      if (C.w_w > 0.0) {
-        double a = 0.0;
-        for (int i = 0; i < 7; ++i) a += ww[i] * ww[i];
-        c += 0.5 * C.w_w * a;
-      }
-      if (C.w_ws > 0.0) {
-        double a = 0.0;
-        for (int i = 0; i < 7; ++i) {
-          const double ov = fabs(ww[i]) - C.ws_lim[i];
-          const double o = ov > 0.0 ? ov : 0.0;
-          a += o * o;
-        }
-        c += C.w_ws * (0.5 * a);
-      }
-    }
-    cost = c;
-  }
-  rec[rec_off_cost(nx)] = cost;
-  for (int r = 0; r < 3; ++r) rec[rec_off_lam(nx) + r] = (mode == MODE_TERMINAL_X) ? 0.0 : P.lam[r];
-  // gaps fs[t+1] = xnext_t - xs[t+1] ; fs[0] = x0 - xs[0]  (zero once feasible)
-  const bool feas = d.st[b].is_feasible != 0;
-  if (!terminal) {
-    double* f = d.fs + ((long)b * (N + 1) + t + 1) * nx;
-    const double* yn = d.xs + ((long)b * (N + 1) + t + 1) * nx;
-    for (int i = 0; i < 14; ++i) f[i] = feas ? 0.0 : P.xnext[i] - yn[i];
-    if (FF) {
-      const double* wv = d.us + ((long)b * N + t) * NU;
-      for (int i = 0; i < 7; ++i) f[14 + i] = feas ? 0.0 : (C.alpha * y[14 + i] + C.beta * wv[i]) - yn[14 + i];
-    }
-  }
-  if (t == 0) {
-    double* f = d.fs + (long)b * (N + 1) * nx;
-    for (int i = 0; i < nx; ++i) f[i] = feas ? 0.0 : x0[(long)b * nx + i] - y[i];
-  }
-}
-
 // k_primal on 8-lane groups (ffddp_primal_g8.hpp): one group per node, the
 // rigid-body recursions as log-depth scans; same outputs as k_primal.
 template <int NC, bool FF>
@@ -311,6 +226,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_G8_WA
   }
 }
 
+// a^T H b over the contact-force block of the Gauss-Newton Hessian: diagonal
+// Dd plus (nc = 3) the friction cone's off-diagonal couplings Do
+template <int NC>
+__device__ __forceinline__ double fquad(const double* a, const double* Dd, const double* Do, const double* b) {
+  double acc = 0.0;
+#pragma unroll
+  for (int r = 0; r < NC; ++r) acc += a[r] * Dd[r] * b[r];
+  if (NC == 3)
+    acc += Do[0] * (a[1] * b[0] + a[0] * b[1]) + Do[1] * (a[2] * b[0] + a[0] * b[2]) +
+           Do[2] * (a[2] * b[1] + a[1] * b[2]);
+  return acc;
+}
+
 // calcDiff tangents + Gauss-Newton assembly: 16-lane group per node
 template <int NC, bool FF>
 __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE_WAVES))) void k_node(const DevConsts* __restrict__ Cg, Dev d,
@@ -349,11 +277,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
   double da[NQ], dlam[3], col[NDENSE_MAX];
   double dau[NQ], dlamu[3];
   if (active && lane < 14) {
-#ifdef FFDDP_DUAL_TANGENT
-    node_tangent_state<NC>(C, mode, surf, y, ref, P, lane, da, dlam, col);
-#else
     node_tangent_state_an<NC>(C, mode, surf, G.lk, P, lane, da, dlam, col);
-#endif
   }
   if (active && lane < 7 && need_u) node_tangent_control<NC>(C, surf, P, lane, dau, dlamu);
   __syncthreads();  // every lane's reads of lk are done before col overwrites it
@@ -378,7 +302,8 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
       double* Lxx = rec + rec_off_Lxx(nx);
       for (int i = 0; i < 14; ++i) {
         double acc = 0.0;
-        for (int r = 0; r < nd; ++r) acc += G.col[i][r] * D[r] * col[r];
+        for (int r = 0; r < 12; ++r) acc += G.col[i][r] * D[r] * col[r];
+        acc += fquad<NC>(&G.col[i][12], D + 12, P.Dfo, col + 12);
         if (i == j) acc += P.Dx[j];
         acc *= sc;
         if (ff && i == j) acc += C.w_y * C.Wy2[j];
@@ -394,7 +319,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
       if (need_u) {
         for (int kk = 0; kk < NU; ++kk) {
           double acc = 0.0;
-          for (int r = 0; r < nc; ++r) acc += col[12 + r] * D[12 + r] * G.colu[kk][r];
+          acc = fquad<NC>(col + 12, D + 12, P.Dfo, G.colu[kk]);
           acc *= sc;
           if (ff)
             Lxx[(14 + kk) * nx + j] = acc;
@@ -410,7 +335,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
       double luu[7];
       for (int m = 0; m < NU; ++m) {
         double acc = 0.0;
-        for (int r = 0; r < nc; ++r) acc += G.colu[m][r] * D[12 + r] * G.colu[kk][r];
+        acc = fquad<NC>(G.colu[m], D + 12, P.Dfo, G.colu[kk]);
         if (m == kk) acc += P.Du[kk];
         luu[m] = acc * sc;
       }
@@ -425,7 +350,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
         // Lxx_aug column 14+kk: rows 0..13 = Lxu_in[:, kk], rows 14..20 = Luu_in[:, kk] + w_y Wy2
         for (int i = 0; i < 14; ++i) {
           double acc = 0.0;
-          for (int r = 0; r < nc; ++r) acc += G.col[i][12 + r] * D[12 + r] * G.colu[kk][r];
+          acc = fquad<NC>(&G.col[i][12], D + 12, P.Dfo, G.colu[kk]);
           Lxx[i * nx + 14 + kk] = acc * sc;
         }
         for (int m = 0; m < NU; ++m)
@@ -450,487 +375,14 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
   }
 }
 
-// ---------------------------------------------------------------------------
-// backward pass (SolverDDP::backwardPass + SolverBoxFDDP::computeGains)
-//
-// Column-per-lane layout: a group of G lanes (G = 16 for nx = 14, 32 for
-// nx = 21) owns one instance; lane j keeps column j of V_xx in registers and
-// computes column j of T1 = Fx^T V_xx', Q_xx, K and the new V_xx.  Fx / Fu are
-// never materialised: with the Euler structure
-//   Fx = I + [[dt^2 A_x],[dt A_x]] + [[0, dt I],[0, 0]],  Fu = [[dt^2 A_u],[dt A_u]]
-// (FF: extra rows [0, alpha I] / [beta I]) every product is a 7-deep
-// contraction with the node's acceleration Jacobian A (half the flops of the
-// dense 14x14x14 products).  One wavefront = 64/G instances; the serial gains
-// (LLT or BoxQP) of those instances run concurrently on their group leaders.
-// ---------------------------------------------------------------------------
-constexpr int NXM = 21;
 
 __device__ __forceinline__ bool bad(double v) { return isnan(v) || isinf(v) || v >= 1e30; }
 
-// BoxQP (crocoddyl::BoxQP::solve), one lane, everything in registers.
-// The free-set sub-problem is solved on the full 7x7 matrix with clamped
-// rows/columns replaced by identity rows (the same Cholesky as on H_ff); the
-// factorisation is reused while the free set does not change.
-// H (row-major 7x7), q, lb, ub; x: in = warm start, out = solution.
-// L: masked factor of the final free set (so that K = Quu_ff^-1 Qxu_f^T is
-// a masked solve), clamped: final clamped flags.  Returns false on LLT
-// failure ("backward_error").
-__device__ __forceinline__ bool boxqp_reg(const DevConsts& C, const double* __restrict__ H, const double (&q)[NU],
-                                          const double (&lb)[NU], const double (&ub)[NU], double (&x)[NU],
-                                          double (&L)[28], bool (&clamped)[NU]) {
-#pragma unroll
-  for (int i = 0; i < NU; ++i) x[i] = fmax(fmin(x[i], ub[i]), lb[i]);
-  bool have = false;
-  double xs_f[NU];  // free-set Newton target for the current free set (cached)
-#pragma unroll 1
-  for (int it = 0; it < C.qp_maxiter; ++it) {
-    double g[NU];
-#pragma unroll
-    for (int i = 0; i < NU; ++i) {
-      double acc = q[i];
-#pragma unroll
-      for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * x[j];
-      g[i] = acc;
-    }
-    bool changed = !have;
-#pragma unroll
-    for (int j = 0; j < NU; ++j) {
-      const bool c = (x[j] == lb[j] && g[j] > 0.0) || (x[j] == ub[j] && g[j] < 0.0);
-      changed |= (c != clamped[j]);
-      clamped[j] = c;
-    }
-    if (changed) {
-      // new free set: refactor and re-solve.  While the free set is unchanged
-      // the clamped x stay at their bounds, so the right-hand side
-      // -q_f - H_fc x_c and hence the Newton target are unchanged.
-#pragma unroll
-      for (int i = 0; i < NU; ++i)
-#pragma unroll
-        for (int j = 0; j <= i; ++j)
-          L[tri(i, j)] = (!clamped[i] && !clamped[j]) ? H[i * NU + j] + (i == j ? C.qp_reg : 0.0)
-                                                      : (i == j ? 1.0 : 0.0);
-      if (!chol_packed<NU>(L)) return false;
-      have = true;
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        double acc = -q[i];
-#pragma unroll
-        for (int j = 0; j < NU; ++j)
-          if (clamped[j]) acc -= H[i * NU + j] * x[j];
-        xs_f[i] = clamped[i] ? 0.0 : acc;
-      }
-      chol_solve<NU>(L, xs_f);
-    }
-    double dx[NU];
-#pragma unroll
-    for (int i = 0; i < NU; ++i) dx[i] = xs_f[i];
-    double dmax = 0.0;
-#pragma unroll
-    for (int i = 0; i < NU; ++i) {
-      dx[i] = clamped[i] ? 0.0 : dx[i] - x[i];
-      dmax = fmax(dmax, fabs(dx[i]));
-    }
-    if (dmax < C.qp_th_grad) break;
-    double fold;
-    {
-      double a1 = 0.0, a2 = 0.0;
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * x[j];
-        a1 += x[i] * acc;
-        a2 += q[i] * x[i];
-      }
-      fold = 0.5 * a1 + a2;
-    }
-#pragma unroll 1
-    for (int ia = 0; ia < NTRIALS; ++ia) {
-      const double al = C.alphas[ia];
-      double xn[NU];
-#pragma unroll
-      for (int i = 0; i < NU; ++i) xn[i] = fmax(fmin(x[i] + al * dx[i], ub[i]), lb[i]);
-      double a1 = 0.0, a2 = 0.0, gd = 0.0;
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < NU; ++j) acc += H[i * NU + j] * xn[j];
-        a1 += xn[i] * acc;
-        a2 += q[i] * xn[i];
-        gd += g[i] * (x[i] - xn[i]);
-      }
-      if (fold - (0.5 * a1 + a2) > C.qp_th_acceptstep * gd) {
-#pragma unroll
-        for (int i = 0; i < NU; ++i) x[i] = xn[i];
-        break;
-      }
-    }
-  }
-  return true;
-}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
-}
-
-template <int G> __device__ __forceinline__ double group_sum(double v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-template <int G> __device__ __forceinline__ int group_or(int v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v |= __shfl_xor(v, o);
-  return v;
-}
-
-template <bool FF> struct BwGroup {
-  static constexpr int NX = FF ? 21 : 14;
-  double A[21 * 7];  // A[dir][comp]
-  double T1[NX * NX];
-  double Z[NX * 7];  // Z[i][m] = dt^2 T1[i][m] + dt T1[i][m+7]
-  double Qxx[NX * NX];
-  double Qxu[NX * 7];
-  double T2[7 * NX];
-  double Quu[49];
-  double L[28];
-  double K[7 * NX];  // K[c][j]
-  double Vxx[NX * NX];  // V_xx' (column j written/read by lane j only)
-  double Qu[7], kk[7], fs[NX], Vx[NX], Qx[NX];
-  int flag;
-  int clamped[7];
-};
-
-template <bool FF>
-__global__ __launch_bounds__(BW_BLOCK) void k_backward(const DevConsts* __restrict__ Cg, Dev d, int iter) {
-  constexpr int NX = FF ? 21 : 14;
-  constexpr int G = FF ? 32 : 16;
-  constexpr int IPB = BW_BLOCK / G;
-  const DevConsts& C = *Cg;
-  const int N = C.N;
-  __shared__ BwGroup<FF> SS[IPB];
-  const int grp = threadIdx.x / G, j = threadIdx.x % G;
-  const int b = blockIdx.x * IPB + grp;
-  BwGroup<FF>& S = SS[grp];
-  bool finished = true;
-  InstState* st = nullptr;
-  if (b < d.B) {
-    st = d.st + b;
-    finished = st->done != 0;
-  }
-  const bool active = !finished;
-  const bool feas = active ? st->is_feasible != 0 : true;
-#ifdef FFDDP_EXP_NOQP
-  const bool use_qp = false;  // ablation build only (timing experiment)
-#else
-  const bool use_qp = C.use_box && feas;
-#endif
-  const double dt = C.dt, dt2 = C.dt * C.dt;
-  const double* recb = d.rec_buf + (long)(active ? b : 0) * (N + 1) * d.rec;
-  const int rec = d.rec;
-  if (active && j == 0 && st->recalc) {
-    // ShootingProblem::calcDiff cost, summed over t = 0..N
-    double c = 0.0;
-    for (int t = 0; t <= N; ++t) c += recb[(long)t * rec + rec_off_cost(NX)];
-    st->cost = c;
-    st->n_calc += 1;
-  }
-  double preg = active ? st->preg : 0.0;
-  int retries = 0;
-  bool fail_inst = false;
-  double dg = 0.0, dq = 0.0, stop = 0.0;
-  for (;;) {
-    bool failed = false;
-    const bool work0 = !finished;
-    dg = dq = stop = 0.0;
-    double vx_j = 0.0;
-    // ---- terminal node: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N) ----
-    if (work0 && j < NX) {
-      const double* rT = recb + (long)N * rec;
-      const double* fsN = d.fs + ((long)b * (N + 1) + N) * NX;
-      double vfs = 0.0;
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        const double v = rT[rec_off_Lxx(NX) + i * NX + j] + (i == j ? preg : 0.0);
-        S.Vxx[i * NX + j] = v;
-        vfs += v * fsN[i];
-      }
-      const double fj = fsN[j];
-      vx_j = rT[rec_off_Lx(NX) + j] + (feas ? 0.0 : vfs);
-      if (!feas) {
-        d.w[((long)b * (N + 1) + N) * NX + j] = vfs;
-        dg -= vx_j * fj;
-        dq += fj * vfs;
-      }
-      S.Vx[j] = vx_j;
-    }
-    __syncthreads();
-    for (int t = N - 1; t >= 0; --t) {
-      const bool work = work0 && !failed;
-      const double* r = recb + (long)t * rec;
-      if (work) {
-        for (int e = j; e < 147; e += G) S.A[e] = r[rec_off_A() + e];
-        if (j < NX) S.fs[j] = d.fs[((long)b * (N + 1) + t) * NX + j];
-      }
-      __syncthreads();
-      if (work && j < NX) {
-        // ---- T1 = Fx^T Vxx' (column j), T2 = Fu^T Vxx' (column j), Qx ----
-        double Vcol[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) Vcol[i] = S.Vxx[i * NX + j];
-        double W[7];
-#pragma unroll
-        for (int m = 0; m < 7; ++m) W[m] = dt2 * Vcol[m] + dt * Vcol[m + 7];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-          double acc = (i < 14) ? Vcol[i] : C.alpha * Vcol[i];
-          if (i >= 7 && i < 14) acc += dt * Vcol[i - 7];
-#pragma unroll
-          for (int m = 0; m < 7; ++m) acc += S.A[i * 7 + m] * W[m];
-          S.T1[i * NX + j] = acc;
-        }
-#pragma unroll
-        for (int c = 0; c < 7; ++c) {
-          double acc;
-          if (FF) {
-            acc = C.beta * Vcol[14 + c];
-          } else {
-            acc = 0.0;
-#pragma unroll
-            for (int m = 0; m < 7; ++m) acc += S.A[(14 + c) * 7 + m] * W[m];
-          }
-          S.T2[c * NX + j] = acc;
-        }
-      }
-      __syncthreads();
-      if (work && j < NX) {
-        double Arow[7];
-#pragma unroll
-        for (int m = 0; m < 7; ++m) Arow[m] = S.A[j * 7 + m];
-        double wv[7];
-#pragma unroll
-        for (int m = 0; m < 7; ++m) wv[m] = dt2 * S.Vx[m] + dt * S.Vx[m + 7];
-        double qx_j = r[rec_off_Lx(NX) + j] + ((j < 14) ? S.Vx[j] : C.alpha * S.Vx[j]);
-        if (j >= 7 && j < 14) qx_j += dt * S.Vx[j - 7];
-#pragma unroll
-        for (int m = 0; m < 7; ++m) qx_j += Arow[m] * wv[m];
-        S.Qx[j] = qx_j;
-        if (j < 7) {
-          double qu = r[rec_off_Lu(NX) + j];
-          if (FF) {
-            qu += C.beta * S.Vx[14 + j];
-          } else {
-#pragma unroll
-            for (int m = 0; m < 7; ++m) qu += S.A[(14 + j) * 7 + m] * wv[m];
-          }
-          S.Qu[j] = qu;
-        }
-        // Z row j
-#pragma unroll
-        for (int m = 0; m < 7; ++m) S.Z[j * 7 + m] = dt2 * S.T1[j * NX + m] + dt * S.T1[j * NX + m + 7];
-      }
-      __syncthreads();
-      if (work && j < NX) {
-        // ---- Qxx column j = Lxx + T1 Fx ; Qxu row j = Lxu + T1 Fu ; Quu column j ----
-        double Arow[7];
-#pragma unroll
-        for (int m = 0; m < 7; ++m) Arow[m] = S.A[j * 7 + m];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-          double acc = r[rec_off_Lxx(NX) + i * NX + j];
-          acc += (j < 14) ? S.T1[i * NX + j] : C.alpha * S.T1[i * NX + j];
-          if (j >= 7 && j < 14) acc += dt * S.T1[i * NX + j - 7];
-#pragma unroll
-          for (int m = 0; m < 7; ++m) acc += S.Z[i * 7 + m] * Arow[m];
-          S.Qxx[i * NX + j] = acc;
-        }
-#pragma unroll
-        for (int c = 0; c < 7; ++c) {
-          double acc = r[rec_off_Lxu(NX) + j * 7 + c];
-          if (FF) {
-            acc += C.beta * S.T1[j * NX + 14 + c];
-          } else {
-#pragma unroll
-            for (int m = 0; m < 7; ++m) acc += S.Z[j * 7 + m] * S.A[(14 + c) * 7 + m];
-          }
-          S.Qxu[j * 7 + c] = acc;
-        }
-        if (j < 7) {
-#pragma unroll
-          for (int c = 0; c < 7; ++c) {
-            double acc = r[rec_off_Luu(NX) + c * 7 + j];
-            if (FF) {
-              acc += C.beta * S.T2[c * NX + 14 + j];
-            } else {
-#pragma unroll
-              for (int m = 0; m < 7; ++m)
-                acc += (dt2 * S.T2[c * NX + m] + dt * S.T2[c * NX + m + 7]) * S.A[(14 + j) * 7 + m];
-            }
-            if (c == j) acc += preg;
-            S.Quu[c * 7 + j] = acc;
-          }
-        }
-      }
-      __syncthreads();
-      // ---- gains: Eigen::LLT (infeasible) or BoxQP (feasible, bounded) ----
-      if (work && j == 0) {
-        const double* H = S.Quu;  // stays in LDS (register pressure)
-        bool ok;
-        if (!use_qp) {
-          double L[28];
-#pragma unroll
-          for (int i = 0; i < NU; ++i)
-#pragma unroll
-            for (int jj = 0; jj <= i; ++jj) L[tri(i, jj)] = H[i * NU + jj];
-          ok = chol_packed<NU>(L);
-#pragma unroll
-          for (int e = 0; e < 28; ++e) S.L[e] = L[e];
-#pragma unroll
-          for (int i = 0; i < NU; ++i) S.clamped[i] = 0;
-        } else {
-          const double* kprev = d.k + ((long)b * N + t) * NU;
-          const double* ut = d.us + ((long)b * N + t) * NU;
-          double lb[NU], ub[NU], x[NU], q[NU], L[28];
-          bool cl[NU] = {false, false, false, false, false, false, false};
-#pragma unroll
-          for (int i = 0; i < NU; ++i) {
-            lb[i] = C.u_lb[i] - ut[i];
-            ub[i] = C.u_ub[i] - ut[i];
-            x[i] = kprev[i];
-            q[i] = S.Qu[i];
-          }
-          ok = boxqp_reg(C, H, q, lb, ub, x, L, cl);
-#pragma unroll
-          for (int e = 0; e < 28; ++e) S.L[e] = L[e];
-#pragma unroll
-          for (int i = 0; i < NU; ++i) {
-            S.kk[i] = -x[i];
-            S.clamped[i] = cl[i] ? 1 : 0;
-            if (cl[i]) S.Qu[i] = 0.0;  // BoxFDDP: clamped Qu entries are zeroed
-          }
-        }
-        S.flag = ok ? 0 : 1;
-      }
-      __syncthreads();
-      if (work && S.flag) failed = true;
-      const bool work2 = work && !failed;
-      double Kcol[7];
-      if (work2 && (j < NX || (!use_qp && j == NX))) {
-        if (j < NX) {
-#pragma unroll
-          for (int c = 0; c < 7; ++c) Kcol[c] = S.clamped[c] ? 0.0 : S.Qxu[j * 7 + c];
-        } else {
-#pragma unroll
-          for (int c = 0; c < 7; ++c) Kcol[c] = S.Qu[c];
-        }
-        chol_solve<NU>(S.L, Kcol);
-        if (j < NX) {
-#pragma unroll
-          for (int c = 0; c < 7; ++c) S.K[c * NX + j] = Kcol[c];
-        } else {
-#pragma unroll
-          for (int c = 0; c < 7; ++c) S.kk[c] = Kcol[c];
-        }
-      }
-      __syncthreads();
-      int badv = 0;
-      double c_dg = 0.0, c_dq = 0.0, c_st = 0.0;
-      if (work2 && j < NX) {
-        // ---- Vxx = sym(Qxx - Qxu K) + preg I (column j) ; Vx = Qx - K^T Qu (+ Vxx fs) ----
-        double qxu_j[7];
-#pragma unroll
-        for (int c = 0; c < 7; ++c) qxu_j[c] = S.Qxu[j * 7 + c];
-        double vfs = 0.0;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-          double a1 = S.Qxx[i * NX + j], a2 = S.Qxx[j * NX + i];
-#pragma unroll
-          for (int c = 0; c < 7; ++c) {
-            a1 -= S.Qxu[i * 7 + c] * Kcol[c];
-            a2 -= qxu_j[c] * S.K[c * NX + i];
-          }
-          const double v = 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
-          S.Vxx[i * NX + j] = v;
-          vfs += v * S.fs[i];
-          badv |= bad(fabs(v)) ? 1 : 0;
-        }
-        double vx = S.Qx[j];
-#pragma unroll
-        for (int c = 0; c < 7; ++c) vx -= Kcol[c] * S.Qu[c];
-        if (!feas) vx += vfs;
-        badv |= bad(fabs(vx)) ? 1 : 0;
-        vx_j = vx;
-        double* Kt = d.K + ((long)b * N + t) * NU * NX;
-#pragma unroll
-        for (int c = 0; c < 7; ++c) Kt[c * NX + j] = Kcol[c];
-        if (!feas) {
-          d.w[((long)b * (N + 1) + t) * NX + j] = vfs;
-          c_dg -= vx * S.fs[j];
-          c_dq += S.fs[j] * vfs;
-        }
-        if (j < 7) {
-          double quk = 0.0;
-#pragma unroll
-          for (int m = 0; m < 7; ++m) quk += S.Quu[j * 7 + m] * S.kk[m];
-          c_dg += S.Qu[j] * S.kk[j];
-          c_dq -= S.kk[j] * quk;
-          c_st += S.Qu[j] * S.Qu[j];
-          d.k[((long)b * N + t) * NU + j] = S.kk[j];
-        }
-      }
-      badv = group_or<G>(badv);
-      c_dg = group_sum<G>(c_dg);
-      c_dq = group_sum<G>(c_dq);
-      c_st = group_sum<G>(c_st);
-      __syncthreads();
-      if (work2) {
-        if (badv) {
-          failed = true;
-        } else {
-          dg += c_dg;
-          dq += c_dq;
-          stop += c_st;
-          if (j < NX) S.Vx[j] = vx_j;
-        }
-      }
-      __syncthreads();
-    }
-    // ---- retry bookkeeping (SolverFDDP::solve: increaseRegularization) ----
-    if (!finished) {
-      if (failed) {
-        retries++;
-        preg = fmin(preg * C.reg_inc, C.reg_max);
-        if (preg == C.reg_max) {
-          finished = true;
-          fail_inst = true;
-        }
-      } else {
-        finished = true;
-      }
-    }
-    if (__syncthreads_and(finished ? 1 : 0)) break;
-  }
-  if (active && j == 0) {
-    st->preg = preg;
-    st->n_retries += retries;
-    if (fail_inst) {
-      st->bw_ok = 0;
-      st->iter = iter;
-      st->done = 1;
-      st->ok = 0;
-      st->n_backward += retries;
-    } else {
-      st->dg = dg;
-      st->dq = dq;
-      st->stop = stop;
-      st->bw_ok = 1;
-      st->n_backward += retries + 1;
-      st->n_iters += 1;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1183,11 +635,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
   PP_INIT();
   __shared__ S_t S;
   const bool feas = st->is_feasible != 0;
-#ifdef FFDDP_EXP_NOQP
-  const bool use_qp = false;
-#else
   const bool use_qp = C.use_box && feas;
-#endif
   const double dt = C.dt, dt2 = C.dt * C.dt, alpha = C.alpha, beta = C.beta;
   const double* recb = d.rec_buf + (long)b * (N + 1) * REC;
   if (st->recalc) {
@@ -1523,81 +971,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
 }
 
 // ---------------------------------------------------------------------------
-// line search: one lane per (instance, step length)
-// ---------------------------------------------------------------------------
-template <int NC, bool FF>
-__global__ __launch_bounds__(FW_BLOCK) void k_forward(const DevConsts* __restrict__ Cg, Dev d,
-                                                       const double* __restrict__ x0,
-                                                       const double* __restrict__ node_ref,
-                                                       const double* __restrict__ inst_ref,
-                                                       const uint8_t* __restrict__ surface) {
-  const DevConsts& C = *Cg;
-  const int N = C.N;
-  constexpr int nx = FF ? 21 : 14;
-  const long gid = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const int b = (int)(gid / NTRIALS), tr = (int)(gid % NTRIALS);
-  if (b >= d.B) return;
-  const InstState* st = d.st + b;
-  if (st->done) return;
-  const double alpha = C.alphas[tr];
-  const bool feas = st->is_feasible != 0;
-  const bool gap = !(feas || alpha == 1.0);
-  const bool surf = surface[b] != 0;
-  const double* xreg = inst_ref + (long)b * 21;
-  const double* tauref = xreg + 14;
-  const double* yref = x0 + (long)b * nx;
-  double xh[21], xt[21], u[NU];
-  for (int i = 0; i < nx; ++i) xh[i] = x0[(long)b * nx + i];
-  double cost = 0.0, dv = 0.0;
-  bool fail = false;
-  double* xtr = d.xs_try + ((long)b * NTRIALS + tr) * (N + 1) * nx;
-  double* utr = d.us_try + ((long)b * NTRIALS + tr) * N * NU;
-  Primal P;
-  for (int t = 0; t <= N; ++t) {
-    const double* xs_t = d.xs + ((long)b * (N + 1) + t) * nx;
-    const double* fs_t = d.fs + ((long)b * (N + 1) + t) * nx;
-    for (int i = 0; i < nx; ++i) xt[i] = gap ? xh[i] + fs_t[i] * (alpha - 1.0) : xh[i];
-    if (!feas) {
-      const double* w_t = d.w + ((long)b * (N + 1) + t) * nx;
-      double acc = 0.0;
-      for (int i = 0; i < nx; ++i) acc += w_t[i] * (xs_t[i] - xt[i]);
-      dv -= acc;
-    }
-    for (int i = 0; i < nx; ++i) xtr[(long)t * nx + i] = xt[i];
-    const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
-    double c;
-    if (t < N) {
-      const double* us_t = d.us + ((long)b * N + t) * NU;
-      const double* K_t = d.K + ((long)b * N + t) * NU * nx;
-      const double* k_t = d.k + ((long)b * N + t) * NU;
-      for (int m = 0; m < NU; ++m) {
-        double acc = us_t[m] - k_t[m] * alpha;
-        for (int i = 0; i < nx; ++i) acc -= K_t[m * nx + i] * (xt[i] - xs_t[i]);
-        if (C.use_box) acc = fmin(fmax(acc, C.u_lb[m]), C.u_ub[m]);
-        u[m] = acc;
-        utr[(long)t * NU + m] = acc;
-      }
-      node_calc<NC, FF>(C, false, surf, xt, u, ref, xreg, tauref, yref, P, xh, c);
-      cost += c;
-      bool xbad = false;
-      for (int i = 0; i < nx; ++i) xbad |= bad(fabs(xh[i]));
-      if (bad(cost) || xbad) {
-        fail = true;
-        break;
-      }
-    } else {
-      double yn[21];
-      node_calc<NC, FF>(C, true, surf, xt, u, ref, xreg, tauref, yref, P, yn, c);
-      cost += c;
-      if (bad(cost)) fail = true;
-    }
-  }
-  d.trial[((long)b * NTRIALS + tr) * 2 + 0] = cost;
-  d.trial[((long)b * NTRIALS + tr) * 2 + 1] = dv;
-  d.trial_fail[(long)b * NTRIALS + tr] = fail ? 1 : 0;
-}
-
-// ---------------------------------------------------------------------------
 // line search with an 8-lane group per (instance, step length): the rollout
 // of one trial is still sequential over the nodes, but each node calc runs
 // joint-parallel (node_calc_g8), which shortens the dependent chain that
@@ -1613,7 +986,9 @@ __device__ __forceinline__ bool trial_accepted(const DevConsts& C, const Dev& d,
   const double d0 = s.dg + dv, d1 = s.dq - 2.0 * dv;
   const double dVexp = a * (d0 + 0.5 * a * d1);
   if (dVexp >= 0) return fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp;
-  return fabs(d0) < C.th_grad || dV > C.th_acceptnegstep * dVexp;  // gap-closing branch
+  // ascent direction (closing gaps may raise the cost): only while infeasible,
+  // accepting a rise of up to th_acceptnegstep x the predicted one
+  return !s.is_feasible && dV > C.th_acceptnegstep * dVexp;
 }
 
 // W: waves/SIMD occupancy target (2 while the batch is throughput-bound, 1 for
@@ -2059,9 +1434,7 @@ struct ffddp_handle {
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
   std::vector<hipEvent_t> stg;  // start-stagger events (FFDDP_STAGGER)
   bool caller_slice = true;  // FFDDP_CALLER_SLICE
-  bool primal_g8 = true;  // calc on 8-lane groups (FFDDP_PRIMAL=lane: one lane per node)
   int stagger = 2;  // 0 off, 1 after the previous slice's node stage, 2 after its primal kernel
-  bool bw_wave = true;
   int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
   // first-pass trial counts of the first iterations (FFDDP_FW_SCHED="2,2,2,2"):
   // while every instance is active the line search is throughput-bound, so a
@@ -2070,7 +1443,6 @@ struct ffddp_handle {
   // instances are done the pass is latency-bound and 4 trials in one pass win
   std::vector<int> fw_sched{2, 2, 2, 2};
   int fw_late_it = 0;  // first iteration using the 1-wave/SIMD line-search variant (FFDDP_FW_LATE_IT)
-  bool fw_group = true;  // 8-lane joint-parallel line search; FFDDP_FW=lane selects one lane per trial  // wave-per-instance backward (FFDDP_BW=group selects the 16-lane-group kernel)
   // optional per-kernel timing
   bool prof = false;
   int prof_mask = 0;
@@ -2154,6 +1526,32 @@ void fill_consts(const ffddp_robot& rb, const ffddp_ocp_config& c, DevConsts& k)
     k.uni_lb[0] = k.uni_lb[1] = -inf;
     k.uni_lb[2] = c.friction_margin;
     k.uni_ub[0] = k.uni_ub[1] = k.uni_ub[2] = inf;
+  }
+  // friction cone (nc = 3 only, crocoddyl_classical.py:678): crocoddyl::FrictionCone
+  // with R = I, nf = 4, inner_appr = false: facet rows (mu_nsurf +- t_i)^T with
+  // t_i = (cos th_i, sin th_i, 0), th_i = i pi / 2, bounds (-inf, 0]; the
+  // normal row e_z with bounds [0, inf); the finite bounds moved inwards by
+  // friction_margin (_make_friction_barrier_activation, :891-903)
+  k.has_fc = (c.nc == 3 && c.w_friction_cone > 0.0) ? 1 : 0;
+  k.w_fc = c.w_friction_cone;
+  {
+    const double eps = c.friction_margin > 0.0 ? c.friction_margin : 0.0;
+    const double theta = 2.0 * M_PI / 4.0;
+    for (int i = 0; i < 2; ++i) {
+      const double ti = theta * (double)i, ct = std::cos(ti), st = std::sin(ti);
+      const double rp[3] = {ct, st, -c.mu}, rm[3] = {-ct, -st, -c.mu};
+      for (int e = 0; e < 3; ++e) {
+        k.fc_A[2 * i][e] = rp[e];
+        k.fc_A[2 * i + 1][e] = rm[e];
+      }
+      k.fc_lb[2 * i] = k.fc_lb[2 * i + 1] = -inf;
+      k.fc_ub[2 * i] = k.fc_ub[2 * i + 1] = 0.0 - eps;
+    }
+    k.fc_A[4][0] = 0.0;
+    k.fc_A[4][1] = 0.0;
+    k.fc_A[4][2] = 1.0;
+    k.fc_lb[4] = 0.0 + eps;
+    k.fc_ub[4] = inf;
   }
   k.has_fn = c.w_fn > 0.0;
   k.w_fn = c.w_fn;
@@ -2350,12 +1748,8 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       if (it == 0 && k > 0 && h->stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
       {
         ProfScope p(h, ss, KC_PRIMAL);
-        if (h->primal_g8)
-          hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k,
-                             nrefk, irefk, surfk, 0);
-        else
-          hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k, nrefk,
-                             irefk, surfk, 0);
+        hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k,
+                           nrefk, irefk, surfk, 0);
       }
       if (it == 0 && h->stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
@@ -2366,14 +1760,10 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       if (it == 0 && h->stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_BACKWARD);
-        if (h->bw_wave)
-          hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it);
-        else
-          hipLaunchKernelGGL((k_backward<FF>), dim3((Bk + (FF ? 1 : 3)) / (FF ? 2 : 4)), dim3(BW_BLOCK), 0, ss, h->dc, d,
-                             it);
+        hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it);
       }
       int n1 = NTRIALS;
-      if (h->fw_group) {
+      {
         // first pass: trials 0..n1-1, per-iteration schedule (fw_sched) then
         // fw_first; the second pass evaluates the rest for the instances that
         // accepted none of them
@@ -2396,10 +1786,6 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
           ProfScope p(h, ss, KC_FORWARD2);
           fw(n1, NTRIALS - n1, 1);
         }
-      } else {
-        ProfScope p(h, ss, KC_FORWARD);
-        hipLaunchKernelGGL((k_forward<NC, FF>), dim3((int)(((long)Bk * NTRIALS + FW_BLOCK - 1) / FW_BLOCK)),
-                           dim3(FW_BLOCK), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk);
       }
       {
         ProfScope p(h, ss, KC_ACCEPT);
@@ -2452,12 +1838,8 @@ int launch_solve(ffddp_handle* h, int B, const double* x0, const double* nref, c
 template <int NC, bool FF>
 void launch_node(ffddp_handle* h, Dev d, int B, hipStream_t s, int force_all) {
   const long nodes = (long)B * (h->hc.N + 1);
-  if (h->primal_g8)
-    hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
-                       h->in_nref, h->in_iref, h->in_surf, force_all);
-  else
-    hipLaunchKernelGGL((k_primal<NC, FF>), dim3((int)((nodes + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
-                       h->in_nref, h->in_iref, h->in_surf, force_all);
+  hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
+                     h->in_nref, h->in_iref, h->in_surf, force_all);
   hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, s, h->dc,
                      d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all);
 }
@@ -2495,15 +1877,11 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     return FFDDP_E_INVALID;
   }
   {
-    const char* bw = std::getenv("FFDDP_BW");
-    h->bw_wave = !(bw && std::strcmp(bw, "group") == 0);
     const char* ns = std::getenv("FFDDP_STREAMS");
     if (ns) {
       const int v = std::atoi(ns);
       h->nstreams = v < 1 ? 1 : (v > 8 ? 8 : v);
     }
-    const char* fw = std::getenv("FFDDP_FW");
-    h->fw_group = !(fw && std::strcmp(fw, "lane") == 0);
     if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
       h->fw_sched.clear();
@@ -2516,7 +1894,6 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     }
     if (const char* sg = std::getenv("FFDDP_STAGGER")) h->stagger = std::atoi(sg);
     if (const char* cs = std::getenv("FFDDP_CALLER_SLICE")) h->caller_slice = std::atoi(cs) != 0;
-    if (const char* pg = std::getenv("FFDDP_PRIMAL")) h->primal_g8 = std::strcmp(pg, "lane") != 0;
     const char* f1 = std::getenv("FFDDP_FW_FIRST");
     if (f1) {
       const int v = std::atoi(f1);

@@ -39,6 +39,9 @@ struct DevConsts {
   double Rdes[9];
   // force costs
   double w_uni, uni_lb[3], uni_ub[3], w_fn, fn_w[3], fn_ref[3];
+  // friction cone (nc = 3): r = A lambda, QuadraticBarrier(lb, ub)
+  int has_fc;
+  double w_fc, fc_A[5][3], fc_lb[5], fc_ub[5];
   // control costs
   double w_tau, w_ts, ts_lb[7], ts_ub[7];
   // contact
@@ -111,6 +114,48 @@ FFD_HD void barrier(double r, double lb, double ub, double& a, double& Ar, doubl
   Arr = (dl <= 0.0 ? 1.0 : 0.0) + (du >= 0.0 ? 1.0 : 0.0);
 }
 
+// Friction-cone cost on the world-aligned contact force lam (nc = 3):
+// ResidualModelContactFrictionCone r = A lam over crocoddyl.FrictionCone(I, mu,
+// nf = 4, inner = False) with a QuadraticBarrier narrowed by friction_margin
+// (crocoddyl_classical.py:678-687, 891-903, 999-1018; FF :959-966).  Returns
+// the weighted cost and, if gl != nullptr, the Gauss-Newton gradient gl[3] =
+// w A^T A_r and Hessian w A^T diag(A_rr) A (diagonal Hd[3], off-diagonal
+// Ho[3] = (1,0), (2,0), (2,1)) in lambda space.
+FFD_HD double friction_cone(const DevConsts& C, const double* lam, double* gl, double* Hd, double* Ho) {
+  double c = 0.0;
+  double g0 = 0.0, g1 = 0.0, g2 = 0.0, h00 = 0.0, h11 = 0.0, h22 = 0.0, h10 = 0.0, h20 = 0.0, h21 = 0.0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const double* A = C.fc_A[k];
+    const double r = A[0] * lam[0] + A[1] * lam[1] + A[2] * lam[2];
+    double ai, Ar, Arr;
+    barrier(r, C.fc_lb[k], C.fc_ub[k], ai, Ar, Arr);
+    c += ai;
+    g0 += A[0] * Ar;
+    g1 += A[1] * Ar;
+    g2 += A[2] * Ar;
+    h00 += A[0] * Arr * A[0];
+    h11 += A[1] * Arr * A[1];
+    h22 += A[2] * Arr * A[2];
+    h10 += A[1] * Arr * A[0];
+    h20 += A[2] * Arr * A[0];
+    h21 += A[2] * Arr * A[1];
+  }
+  if (gl != nullptr) {
+    const double w = C.w_fc;
+    gl[0] = w * g0;
+    gl[1] = w * g1;
+    gl[2] = w * g2;
+    Hd[0] = w * h00;
+    Hd[1] = w * h11;
+    Hd[2] = w * h22;
+    Ho[0] = w * h10;
+    Ho[1] = w * h20;
+    Ho[2] = w * h21;
+  }
+  return C.w_fc * c;
+}
+
 // ---------------------------------------------------------------------------
 // primal
 // ---------------------------------------------------------------------------
@@ -125,8 +170,11 @@ struct Primal {
   double z[NQ][3], o[NQ][3], pee[3], Ree[9];
   double r_rot[3], th_rot;
   // Gauss-Newton data: dense rows 0..2 translation, 3..5 rotation, 6..11
-  // frame velocity (lin, ang), 12.. force;  D = w * A_rr,  g = w * A_r
+  // frame velocity (lin, ang), 12.. force;  D = w * A_rr,  g = w * A_r.
+  // The force block's Hessian is not diagonal once the friction cone couples
+  // the components: Dfo holds its off-diagonal (1,0), (2,0), (2,1) entries.
   double D[NDENSE_MAX], g[NDENSE_MAX];
+  double Dfo[3];
   double Dx[14], gx[14];  // state-residual costs (R_x = I)
   double Du[7], gu[7];    // control-residual costs (R_u = I)
   double cost;            // DAM cost (unscaled)
@@ -171,6 +219,8 @@ FFD_HD void copy_primal(const Primal& s, Primal& d) {
     d.D[i] = s.D[i];
     d.g[i] = s.g[i];
   }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d.Dfo[i] = s.Dfo[i];
 #pragma unroll
   for (int i = 0; i < 14; ++i) {
     d.Dx[i] = s.Dx[i];
@@ -345,6 +395,7 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
   double cost = 0.0;
   #pragma unroll
   for (int k = 0; k < NDENSE_MAX; ++k) P.D[k] = P.g[k] = 0.0;
+  P.Dfo[0] = P.Dfo[1] = P.Dfo[2] = 0.0;
   #pragma unroll
   for (int k = 0; k < 14; ++k) P.Dx[k] = P.gx[k] = 0.0;
   #pragma unroll
@@ -481,6 +532,16 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
     if (mode != MODE_TERMINAL_X)
       #pragma unroll
       for (int r = 0; r < nc; ++r) lam[r] = P.lam[r];
+    if (NC == 3 && C.has_fc) {
+      double gl[3], Hd[3], Ho[3];
+      cost += friction_cone(C, lam, gl, Hd, Ho);
+      #pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        P.D[12 + r] += Hd[r];
+        P.g[12 + r] += gl[r];
+        P.Dfo[r] = Ho[r];
+      }
+    }
     if (C.has_uni) {
       double a = 0.0;
       #pragma unroll
@@ -528,6 +589,8 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
       gout->g[i] = P.g[i];
     }
   #pragma unroll
+    for (int i = 0; i < 3; ++i) gout->Dfo[i] = P.Dfo[i];
+  #pragma unroll
     for (int i = 0; i < 14; ++i) {
       gout->Dx[i] = P.Dx[i];
       gout->gx[i] = P.gx[i];
@@ -539,94 +602,6 @@ FFD_HD void node_primal(const DevConsts& C, int mode, bool surface, const double
       gout->gu[i] = P.gu[i];
     }
     gout->cost = P.cost;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// tangent: state direction j in [0,14) of the inner model
-//   da[7], dlam[nc], col = residual-Jacobian column j over the dense rows
-// ---------------------------------------------------------------------------
-template <int NC>
-FFD_HD void node_tangent_state(const DevConsts& C, int mode, bool surface, const double* x, const double* ref,
-                               const Primal& P, int j, double* da, double* dlam, double* col) {
-  constexpr int nc = NC;
-  const bool with_dyn = mode != MODE_TERMINAL_X;
-  Dual q[NQ], v[NQ];
-  for (int i = 0; i < NQ; ++i) {
-    q[i] = {x[i], i == j ? 1.0 : 0.0};
-    v[i] = {x[NQ + i], NQ + i == j ? 1.0 : 0.0};
-  }
-  RBOut<Dual> K;
-  double fw[3];
-  force_world<NC>(P.lam, fw);
-  if (with_dyn) {
-    rb_pass<Dual, true, false>(C.rb, q, v, P.a, surface ? fw : nullptr, K, nullptr);
-  } else {
-    const double zero[NQ] = {0, 0, 0, 0, 0, 0, 0};
-    rb_pass<Dual, false, false>(C.rb, q, v, zero, nullptr, K, nullptr);
-  }
-  // residual-Jacobian column j over the dense rows
-  const bool isq = j < NQ;
-  double Jl[3] = {0, 0, 0}, wl[3] = {0, 0, 0};
-  if (isq) {
-    // LWA linear Jacobian column z_j x (p - o_j);  local angular R_ee^T z_j
-    const double dx = P.pee[0] - P.o[j][0], dy = P.pee[1] - P.o[j][1], dz = P.pee[2] - P.o[j][2];
-    Jl[0] = P.z[j][1] * dz - P.z[j][2] * dy;
-    Jl[1] = P.z[j][2] * dx - P.z[j][0] * dz;
-    Jl[2] = P.z[j][0] * dy - P.z[j][1] * dx;
-    for (int i = 0; i < 3; ++i) wl[i] = P.Ree[0 * 3 + i] * P.z[j][0] + P.Ree[1 * 3 + i] * P.z[j][1] + P.Ree[2 * 3 + i] * P.z[j][2];
-  }
-  col[0] = Jl[0];
-  col[1] = Jl[1];
-  col[2] = Jl[2];
-  double Jlog[9];
-  jlog3(P.r_rot, P.th_rot, Jlog);
-  for (int i = 0; i < 3; ++i) col[3 + i] = Jlog[3 * i + 0] * wl[0] + Jlog[3 * i + 1] * wl[1] + Jlog[3 * i + 2] * wl[2];
-  col[6] = K.vp.x.d;
-  col[7] = K.vp.y.d;
-  col[8] = K.vp.z.d;
-  col[9] = K.w.x.d;
-  col[10] = K.w.y.d;
-  col[11] = K.w.z.d;
-  for (int r = 0; r < nc; ++r) col[12 + r] = 0.0;
-  for (int i = 0; i < NQ; ++i) da[i] = 0.0;
-  dlam[0] = dlam[1] = dlam[2] = 0.0;
-  if (!with_dyn) return;
-  // dg = d RNEA(q, v, a, fext = lambda) / d x_j  (at fixed a, lambda)
-  double r1[NQ];
-  for (int i = 0; i < NQ; ++i) r1[i] = -K.tau[i].d;
-  if (!surface) {
-    chol_solve<NQ>(P.L, r1);
-    for (int i = 0; i < NQ; ++i) da[i] = r1[i];
-    return;
-  }
-  // dh = d (classical acc + Kp (p - p*) + Kd v_p) / d x_j
-  constexpr int c0 = NC == 1 ? 2 : 0;
-  const double dap[3] = {K.ap.x.d, K.ap.y.d, K.ap.z.d};
-  const double dvp[3] = {K.vp.x.d, K.vp.y.d, K.vp.z.d};
-  const double dpe[3] = {K.pee.x.d, K.pee.y.d, K.pee.z.d};
-  double dh[3];
-  for (int r = 0; r < nc; ++r) dh[r] = dap[c0 + r] + C.Kp * dpe[c0 + r] + C.Kd * dvp[c0 + r];
-  // K [da; -dlam] = -[dg; dh]:  y_l = S^-1 (Jc M^-1 (-dg) + dh), da = M^-1 (-dg - Jc^T y_l), dlam = -y_l
-  double mr[NQ];
-  for (int i = 0; i < NQ; ++i) mr[i] = r1[i];
-  chol_solve<NQ>(P.L, mr);
-  double yl[3];
-  for (int r = 0; r < nc; ++r) {
-    double acc = dh[r];
-    for (int i = 0; i < NQ; ++i) acc += P.Jc[r][i] * mr[i];
-    yl[r] = acc;
-  }
-  chol_solve<NC>(P.Ls, yl);
-  for (int i = 0; i < NQ; ++i) {
-    double acc = r1[i];
-    for (int r = 0; r < nc; ++r) acc -= P.Jc[r][i] * yl[r];
-    da[i] = acc;
-  }
-  chol_solve<NQ>(P.L, da);
-  for (int r = 0; r < nc; ++r) {
-    dlam[r] = -yl[r];
-    col[12 + r] = (mode == MODE_TERMINAL_X) ? 0.0 : dlam[r];
   }
 }
 

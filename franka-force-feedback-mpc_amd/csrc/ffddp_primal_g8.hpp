@@ -523,6 +523,22 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
     if (mode != MODE_TERMINAL_X)
 #pragma unroll
       for (int r = 0; r < NC; ++r) lm[r] = lam[r];
+    if (NC == 3 && C.has_fc) {
+      double gl[3], Hd[3], Ho[3];
+      cee += friction_cone(C, lm, gl, Hd, Ho);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        Dd[12 + r] += Hd[r];
+        gd[12 + r] += gl[r];
+      }
+      if (li == 0) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) gp->Dfo[r] = Ho[r];
+      }
+    } else if (li == 0) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) gp->Dfo[r] = 0.0;
+    }
     if (C.has_uni) {
       double s = 0.0;
 #pragma unroll
@@ -551,6 +567,10 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
 #pragma unroll
     for (int i = 0; i < 3; ++i) gp->r_rot[i] = rr[i];
     gp->th_rot = th;
+    if (!surface) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) gp->Dfo[r] = 0.0;
+    }
   }
   // rows split over the 8 lanes (static indices: lane li stores rows li and li + 8)
 #pragma unroll

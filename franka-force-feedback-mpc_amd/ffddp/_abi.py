@@ -97,6 +97,8 @@ class OcpConfig(C.Structure):
         ("y_weights", C.c_double * 21),
         ("use_inner_state_reg", C.c_int32),
         ("use_inner_tau_reg", C.c_int32),
+        ("w_friction_cone", C.c_double),
+        ("mu", C.c_double),
     ]
 
 

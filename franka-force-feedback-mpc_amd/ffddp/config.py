@@ -41,6 +41,10 @@ class OcpConfig:
     w_vz: float = 5.0e2
     w_unilateral: float = 3.0e1
     friction_margin: float = 1e-3
+    # friction cone (built only for point3d, crocoddyl_classical.py:678); the
+    # benchmark presets switch it off (run_classical.py:292-294: weight 0, mu 1)
+    w_friction_cone: float = 0.0
+    mu: float = 1.0
     w_fn: float = 2.8e1
     fn_des: float = 22.0
     w_wdamp: float = 6.0e1
@@ -77,7 +81,7 @@ class OcpConfig:
             "z_press", "w_ee_pos", "w_ee_ori", "w_posture", "w_v", "w_tau", "w_tau_soft_limits",
             "tau_soft_limit_margin", "w_q_soft_limits", "q_soft_limit_margin", "w_tangent_pos", "w_tangent_vel",
             "w_plane_z", "w_vz", "w_unilateral", "friction_margin", "w_fn", "fn_des", "w_wdamp",
-            "contact_inv_damping", "ff_alpha", "w_w", "w_w_soft_limits", "w_y",
+            "contact_inv_damping", "ff_alpha", "w_w", "w_w_soft_limits", "w_y", "w_friction_cone", "mu",
         ):
             setattr(c, name, float(getattr(self, name)))
         _abi._fill(c.ori_weights, self.ori_weights)

@@ -170,6 +170,7 @@ _OCP_FIELDS = (
     "w_tau_soft_limits", "tau_soft_limit_margin", "w_q_soft_limits", "q_soft_limit_margin", "w_tangent_pos",
     "w_tangent_vel", "w_plane_z", "w_vz", "w_unilateral", "friction_margin", "w_fn", "fn_des", "w_wdamp",
     "w_wdamp_weights", "contact_gains", "contact_inv_damping", "tau_limits", "contact_model", "use_box_fddp",
+    "w_friction_cone", "mu",
 )
 
 
@@ -192,11 +193,6 @@ class _MPCBase:
 
     def __init__(self, sim, traj_fn: Traj, config, device: int = 0):
         cfg = config
-        if float(getattr(cfg, "w_friction_cone", 0.0)) > 0.0:
-            # The reference builds a friction-cone barrier only when this weight is
-            # positive; both benchmark presets set it to 0 and the kernels do not
-            # implement it.
-            raise NotImplementedError("w_friction_cone > 0 is not supported by the HIP OCP kernels")
         self.sim = sim
         self.traj_fn = traj_fn
         self.cfg = cfg

@@ -56,8 +56,6 @@ class FleetClassicalMPC:
         cfg = config
         if int(cfg.mpc_update_steps) != 1 or bool(cfg.apply_command_filter):
             raise NotImplementedError("FleetClassicalMPC supports the benchmark setup: mpc_update_steps=1, no filter")
-        if float(getattr(cfg, "w_friction_cone", 0.0)) > 0.0:
-            raise NotImplementedError("w_friction_cone > 0 is not supported by the HIP OCP kernels")
         self.torch = torch
         self.B, self.cfg, self.traj_fn = int(B), cfg, traj_fn
         self.N = int(cfg.horizon)

@@ -89,6 +89,11 @@ typedef struct ffddp_ocp_config {
   double w_w, w_w_soft_limits, w_y;
   double y_weights[21];
   int32_t use_inner_state_reg, use_inner_tau_reg;
+  /* friction cone, built only for nc = 3 (crocoddyl_classical.py:678-687; FF
+   * crocoddyl_force_feedback.py:959-966): ResidualModelContactFrictionCone over
+   * crocoddyl.FrictionCone(I, mu, nf = 4, inner = False) (:1428-1446) with a
+   * QuadraticBarrier narrowed by friction_margin (:891-903), weight w_friction_cone */
+  double w_friction_cone, mu;
 } ffddp_ocp_config;
 
 /* Task description for the device-side problem builder:

@@ -121,11 +121,29 @@ def boxqp(H, q, lb, ub, xinit, c: Consts):
     return x, free, clamped, Hff_inv
 
 
+def accept_step(c: Consts, is_feasible: bool, dV: float, d0: float, dVexp: float) -> bool:
+    """SolverFDDP::solve step acceptance for one trial.
+    Descent direction (dVexp >= 0): Armijo-like, |d0| < th_grad or
+    dV > th_acceptstep dVexp.  Ascent direction (dVexp < 0, closing the gaps
+    may raise the cost): Crocoddyl 2.x takes this branch only while infeasible
+    (`!is_feasible_ && ...`) and accepts a rise of up to th_acceptnegstep x the
+    predicted one (dV > 2 dVexp, both negative).  SURVEY.md B.1 writes
+    "dV < 2 dVexp"; that rejects the exact LQR step (see
+    tests/test_oracle.py::test_fddp_lqr_known_answer) and DESIGN.md §3 records
+    the choice.  The HIP kernel's trial_accepted is the same rule."""
+    if dVexp >= 0:
+        return abs(d0) < c.th_grad or dV > c.th_acceptstep * dVexp
+    return (not is_feasible) and dV > c.th_acceptnegstep * dVexp
+
+
 @dataclass
 class Stats:
     iters_run: int = 0  # calcDiff+backward executions (I)
     trials: int = 0  # line-search trials a sequential solver executes (L)
     reg_retries: int = 0
+    forward_errors: int = 0  # line-search trials rejected as non-finite (raiseIfNaN)
+    neg_branch: int = 0  # trials judged by the ascent-direction (dVexp < 0) branch
+    clamped: int = 0  # BoxQP solutions with at least one active bound
 
 
 class SolverBoxFDDP:
@@ -198,6 +216,8 @@ class SolverBoxFDDP:
                     Quu_inv[np.ix_(free, free)] = Hff_inv
                 K[t] = Quu_inv @ Qxu.T
                 k[t] = -x
+                if clamped:
+                    self.stats.clamped += 1
                 Qu_t = Qu_t.copy()
                 Qu_t[clamped] = 0.0
             Vx_t = Qx - K[t].T @ Qu_t
@@ -303,18 +323,14 @@ class SolverBoxFDDP:
                 try:
                     xs_try, us_try, cost_try = self._forward(steplength)
                 except ForwardError:
+                    self.stats.forward_errors += 1
                     continue
                 dV = self.cost - cost_try
                 d0, d1 = self._expected_improvement(xs_try)
                 dVexp = steplength * (d0 + 0.5 * steplength * d1)
-                if dVexp >= 0:
-                    ok = abs(d0) < c.th_grad or dV > c.th_acceptstep * dVexp
-                else:
-                    # gap-closing branch: accept a cost increase of up to
-                    # th_acceptnegstep x the predicted one.  (SURVEY.md B.1 writes
-                    # "dV < 2 dVexp"; that rejects the exact LQR step — see
-                    # tests/test_oracle.py::test_fddp_lqr_known_answer.)
-                    ok = abs(d0) < c.th_grad or dV > c.th_acceptnegstep * dVexp
+                if dVexp < 0:
+                    self.stats.neg_branch += 1
+                ok = accept_step(c, self.is_feasible, dV, d0, dVexp)
                 if ok:
                     self.was_feasible = self.is_feasible
                     self.xs, self.us = xs_try, us_try

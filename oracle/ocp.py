@@ -68,6 +68,8 @@ class OCPConfig:
     w_vz: float = 5.0e2
     w_unilateral: float = 3.0e1
     friction_margin: float = 1e-3
+    w_friction_cone: float = 0.0  # run_classical.py:292 (benchmark presets: off)
+    mu: float = 1.0  # run_classical.py:294
     w_fn: float = 2.8e1
     fn_des: float = 22.0
     w_wdamp: float = 6.0e1
@@ -263,6 +265,32 @@ def dynamics_derivatives(cfg, q, v, dyn, surface, p_star):
     return dict(Fx=Fx, Fu=Kaa, dfdx=dfdx, dfdu=-Kla)
 
 
+def friction_cone(cfg):
+    """crocoddyl.FrictionCone(R=I, mu, nf=4, inner_appr=False) as the reference
+    builds it (crocoddyl_classical.py:1428-1446; Crocoddyl 2.x FrictionCone::update:
+    facet rows (-mu e_z +- t_i)^T R^T with t_i = (cos th_i, sin th_i, 0),
+    th_i = i 2 pi / nf, bounds (-inf, 0]; row nf = R e_z with bounds
+    [min_nforce = 0, inf)), and the barrier bounds of
+    _make_friction_barrier_activation (:891-903): finite bounds moved inwards by
+    friction_margin."""
+    nf = 4
+    theta = 2.0 * np.pi / nf
+    A = np.zeros((nf + 1, 3))
+    for i in range(nf // 2):
+        t = np.array([np.cos(theta * i), np.sin(theta * i), 0.0])
+        mn = np.array([0.0, 0.0, -cfg.mu])
+        A[2 * i] = mn + t
+        A[2 * i + 1] = mn - t
+    A[nf] = [0.0, 0.0, 1.0]
+    lb = np.full(nf + 1, -INF)
+    ub = np.zeros(nf + 1)
+    lb[nf], ub[nf] = 0.0, INF
+    eps = max(cfg.friction_margin, 0.0)
+    lb = np.where(np.isfinite(lb), lb + eps, lb)
+    ub = np.where(np.isfinite(ub), ub - eps, ub)
+    return A, lb, ub
+
+
 def cost_stack(cfg, surface, terminal):
     """Ordered cost list of _make_dam (crocoddyl_classical.py:567-718).
 
@@ -292,6 +320,9 @@ def cost_stack(cfg, surface, terminal):
     if cfg.w_vz > 0.0:
         costs.append(("vz_damp", ("frame_vel", "zero"), cfg.w_vz, ("wquad", np.array([0.0, 0, 1, 0, 0, 0]))))
     nc = cfg.nc
+    if nc == 3 and cfg.w_friction_cone > 0.0:
+        A, lb, ub = friction_cone(cfg)
+        costs.append(("friction_cone", ("force_cone", A), cfg.w_friction_cone, ("barrier", lb, ub)))
     if cfg.w_unilateral > 0.0:
         if nc == 1:
             lb, ub = np.array([cfg.friction_margin]), np.array([INF])
@@ -385,6 +416,20 @@ def dam_eval(cfg, prob_refs, x, u, surface, mode, diff):
             r = v_frame - ref
             if diff:
                 Rx = dvel
+        elif kind[0] == "force_cone":
+            # ResidualModelContactFrictionCone: r = A lambda (world-aligned force)
+            A = kind[1]
+            if mode == "terminal_x" or not surface:
+                lam = np.zeros(batch + (nc,))
+            else:
+                lam = dyn["lam"]
+            r = np.einsum("kr,...r->...k", A, lam)
+            if diff:
+                if mode == "terminal_x":
+                    Rx = np.zeros(batch + (A.shape[0], 14))
+                else:
+                    Rx = np.einsum("kr,...ri->...ki", A, ddyn["dfdx"])
+                    Ru = np.einsum("kr,...ri->...ki", A, ddyn["dfdu"])
         elif kind[0] == "force":
             fref = kind[1]
             if mode == "terminal_x" or not surface:

@@ -53,3 +53,19 @@ def oracle_solve(cfg: OcpConfig, batch, i, maxiter=10, box=True):
 def rel_err(a, b):
     a, b = np.asarray(a, float), np.asarray(b, float)
     return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def log_parity(case: str, **fields):
+    """Append one JSON line with the observed errors of a parity case to
+    $FFDDP_PARITY_LOG (when set), so the tolerances can be set from data."""
+    import json
+    import os
+
+    path = os.environ.get("FFDDP_PARITY_LOG")
+    if not path:
+        return
+    rec = {"case": case}
+    for k, v in fields.items():
+        rec[k] = v.item() if hasattr(v, "item") else v
+    with open(path, "a") as f:
+        f.write(json.dumps(rec) + "\n")

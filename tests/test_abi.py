@@ -90,3 +90,26 @@ def test_null_handle_errors():
     lib = _abi.load()
     assert lib.ffddp_profile_enable(None, 1) == -1
     assert b"null" in lib.ffddp_last_error(None)
+
+
+def test_integration_snippet_matches_header():
+    """INTEGRATION.md §2's ctypes binding: argtypes follow the header's
+    ffddp_solve_batch signature and the stats buffer holds FFDDP_NSTATS words
+    per instance (the library writes B * FFDDP_NSTATS int32)."""
+    doc = (ROOT / "INTEGRATION.md").read_text()
+    block = doc.split("## 2. ")[1].split("```python")[1].split("```")[0]
+    hdr = HEADER.read_text()
+    nstats = int(re.search(r"#define FFDDP_NSTATS (\d+)", hdr).group(1))
+    assert nstats == _abi.NSTATS
+    assert int(re.search(r"^FFDDP_NSTATS = (\d+)", block, re.M).group(1)) == nstats
+    assert re.search(r"stats = np\.zeros\(\(1, FFDDP_NSTATS\), np\.int32\)", block)
+    # argtypes vs the C prototype, parameter by parameter
+    ns = {"C": ctypes, "D": ctypes.POINTER(ctypes.c_double), "I32": ctypes.POINTER(ctypes.c_int32),
+          "U8": ctypes.POINTER(ctypes.c_uint8)}
+    m = re.search(r"lib\.ffddp_solve_batch\.argtypes = (\[.*?\])", block, re.S)
+    doc_types = eval(m.group(1), ns)  # noqa: S307 (our own documentation text)
+    proto = re.search(r"int ffddp_solve_batch\((.*?)\);", hdr, re.S).group(1)
+    cmap = {"ffddp_handle*": ctypes.c_void_p, "int": ctypes.c_int, "const double*": ns["D"], "double*": ns["D"],
+            "const uint8_t*": ns["U8"], "uint8_t*": ns["U8"], "int32_t*": ns["I32"]}
+    params = [" ".join(p.split()[:-1]).replace(" *", "*") for p in proto.replace("\n", " ").split(",")]
+    assert [cmap[p] for p in params] == doc_types

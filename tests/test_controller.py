@@ -51,6 +51,7 @@ class OracleSolver:
     def __init__(self, cfg, max_batch, device=0):
         self.cfg = cfg
         self.N = cfg.horizon
+        OracleSolver.last_cfg = cfg
 
     def solve(self, batch, maxiter=10, is_feasible=False, xs_init=None, us_init=None):
         N = self.N
@@ -145,10 +146,20 @@ def test_mode_switch_invalidates_warm_start(monkeypatch):
     assert np.isfinite(c.last_info["fn_pred"])
 
 
-def test_friction_cone_rejected(monkeypatch):
+@pytest.mark.parametrize("contact_model", ["normal_1d", "point3d"])
+def test_default_config_builds_with_friction_cone(monkeypatch, contact_model):
+    """ClassicalMPCConfig() (w_friction_cone = 2e2, mu = 0.6) builds like the
+    reference's; the cone weight and mu reach the OCP, which adds the cone only
+    for nc = 3 (crocoddyl_classical.py:678)."""
     monkeypatch.setattr(CT, "BatchedBoxFDDP", OracleSolver)
-    with pytest.raises(NotImplementedError):
-        CT.ClassicalCrocoddylMPC(FakeSim(R.Q_NEUTRAL), _traj(), CT.ClassicalMPCConfig())
+    cfg = CT.ClassicalMPCConfig(contact_model=contact_model, horizon=4, max_iters=2)
+    c = CT.ClassicalCrocoddylMPC(FakeSim(R.Q_NEUTRAL), _traj(), cfg)
+    tau = c.compute_control(c.sim.get_observation(), 1.0)
+    assert np.all(np.isfinite(tau))
+    ocfg = oracle_cfg(c._solver.cfg)
+    assert ocfg.w_friction_cone == 2.0e2 and ocfg.mu == 0.6
+    names = [n for n, *_ in ocp.cost_stack(ocfg, surface=True, terminal=False)]
+    assert ("friction_cone" in names) == (contact_model == "point3d")
 
 
 @pytest.mark.gpu

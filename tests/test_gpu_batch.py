@@ -18,7 +18,8 @@ import pytest
 
 from ffddp import BatchedBoxFDDP, FfddpError
 
-from helpers import make_batch, oracle_cfg, oracle_problem, oracle_solve, product_cfg, rel_err
+from helpers import log_parity, make_batch, oracle_cfg, oracle_problem, oracle_solve, product_cfg, rel_err
+from oracle_pool import solve_many
 
 pytestmark = pytest.mark.gpu
 
@@ -32,11 +33,12 @@ def _sub(batch, idx):
     return b
 
 
-@pytest.mark.parametrize("B", [4096, 517])
-def test_full_batch_equals_small_batches(B, monkeypatch):
+@pytest.mark.parametrize("variant,B", [("classical", 4096), ("classical", 517), ("ff", 1024)])
+def test_full_batch_equals_small_batches(variant, B, monkeypatch):
+    """classical B = 4096: the metric's batch; FF B = 1024: BASELINE configs[2]."""
     N = 30
-    cfg = product_cfg("classical", N)
-    batch = make_batch("classical", B, N, seed=77)
+    cfg = product_cfg(variant, N)
+    batch = make_batch(variant, B, N, seed=77)
     big = BatchedBoxFDDP(cfg, max_batch=B)
     big.solve(batch, maxiter=10)
     # one-stream reference solver for small batches
@@ -52,12 +54,19 @@ def test_full_batch_equals_small_batches(B, monkeypatch):
                 a, b = getattr(big, name)[i], getattr(small, name)[j]
                 assert np.array_equal(a, b, equal_nan=True), (name, int(i))
     # a spread of them against the oracle
-    for i in picks[::4]:
-        ok_o, s = oracle_solve(cfg, batch, int(i))
-        assert bool(big.ok[i]) == bool(ok_o) and int(big.iter[i]) == int(s.iter)
-        assert rel_err(big.xs[i], s.xs) < 1e-6 and rel_err(big.us[i], s.us) < 1e-6
-        assert rel_err(big.cost[i], s.cost) < 1e-6
-    assert np.all(np.isfinite(big.cost)) and np.mean(big.ok) > 0.9
+    sel = picks[::2]
+    ref = solve_many(cfg, batch, sel)
+    e = dict(xs=0.0, us=0.0, cost=0.0)
+    for i, r in zip(sel, ref):
+        assert bool(big.ok[i]) == r["ok"] and int(big.iter[i]) == r["iter"]
+        e["xs"] = max(e["xs"], rel_err(big.xs[i], r["xs"]))
+        e["us"] = max(e["us"], rel_err(big.us[i], r["us"]))
+        e["cost"] = max(e["cost"], rel_err(big.cost[i], r["cost"]))
+    log_parity(f"batch/{variant}/B{B}", n=len(sel), **e)
+    assert max(e.values()) < 1e-10, e  # observed <= 1.3e-11 (profiles/r02_parity_errors.jsonl)
+    assert np.all(np.isfinite(big.cost))
+    if variant == "classical":
+        assert np.mean(big.ok) > 0.9
     big.close()
     small.close()
 

@@ -1,13 +1,21 @@
 """HIP path vs the oracle on identical seeded inputs (run through the C-ABI).
 
-Tolerances (fp64, north_star "stated fp64 tolerance"):
+Tolerances (fp64, north_star "stated fp64 tolerance"), max|gpu - oracle| /
+max(1, max|oracle|) per block:
   * per-node calcDiff blocks (Fx, Fu, Lx, Lu, Lxx, Lxu, Luu, cost, xnext,
-    lambda): max|gpu - oracle| <= 1e-9 * max(1, max|oracle block|)
-    (forward-mode tangents vs complex-step derivatives: two independent
-    exact-derivative methods, agreement limited by rounding only);
-  * full solves: identical discrete path (iterations, ok) and
-    xs / us / K / cost within 1e-6 relative (10 nonlinear iterations
-    amplify rounding differences of the two implementations).
+    lambda): TOL_NODE (closed-form tangents vs complex-step derivatives: two
+    independent exact-derivative methods, agreement limited by rounding);
+  * full solves: IDENTICAL discrete path (iterations, ok, sequential
+    line-search trials, backward passes, regularisation retries) and xs / us
+    / K / cost within TOL_SOLVE (up to 10 nonlinear iterations amplify the
+    rounding differences of two implementations with different evaluation
+    orders).  Every case logs its observed errors to $FFDDP_PARITY_LOG; the
+    tolerances sit about 10x above the largest observed value
+    (profiles/r02_parity_errors.jsonl).
+Cases cover the solver's exceptional paths: BoxQP with active bounds
+(clamped gains), backward-pass failures (regularisation retries),
+non-finite line-search trials, the ascent-direction acceptance branch, the
+friction cone, the SURVEY-literal random x0 at N = 30, plain FDDP and N = 100.
 """
 import numpy as np
 import pytest
@@ -15,27 +23,49 @@ import pytest
 from ffddp import BatchedBoxFDDP
 from oracle import ocp
 
-from helpers import make_batch, oracle_cfg, oracle_problem, oracle_solve, product_cfg, rel_err
+from helpers import log_parity, make_batch, oracle_cfg, oracle_problem, product_cfg, rel_err
+from oracle_pool import solve_many
 
 pytestmark = pytest.mark.gpu
 
-TOL_NODE = 1e-9
-TOL_SOLVE = 1e-6
+# observed maxima (profiles/r02_parity_errors.jsonl): calcDiff blocks <= 9e-14;
+# well-conditioned solves (normal_1d, FF, plain FDDP, clamped, retries)
+# xs/us/cost <= 4e-11, K <= 3e-11.  Contact point3d goes through the 3x3
+# KKT Schur complement with 1e-8 damping (oracle: dense KKT solve), which
+# amplifies rounding differences; those cases carry their own tolerances.
+TOL_NODE = 1e-12
+TOL_SOLVE = 1e-10
+TOL_K = 3e-10
+# case -> (xs/us/cost tolerance, K tolerance), ~10x the observed maxima
+CASE_TOL = {
+    ("classical", "point3d", 1, 0): (6e-9, 7e-8),
+    ("classical", "point3d", 1, 1): (1e-6, 1.2e-7),
+    ("ff", "point3d", 1, 1): (2e-8, 3e-8),
+}
 
 CASES = [
-    ("classical", "normal_1d", 1),
-    ("classical", "normal_1d", 0),
-    ("classical", "point3d", 1),
-    ("ff", "normal_1d", 1),
-    ("ff", "normal_1d", 0),
-    ("ff", "point3d", 1),
+    ("classical", "normal_1d", 1, 0),
+    ("classical", "normal_1d", 0, 0),
+    ("classical", "point3d", 1, 0),
+    ("classical", "point3d", 1, 1),
+    ("ff", "normal_1d", 1, 0),
+    ("ff", "normal_1d", 0, 0),
+    ("ff", "point3d", 1, 0),
+    ("ff", "point3d", 1, 1),
 ]
 
 
-@pytest.mark.parametrize("variant,contact,surf", CASES)
-def test_calc_diff_matches_oracle(variant, contact, surf):
+def _cfg(variant, N, contact, cone=0):
+    c = product_cfg(variant, N, contact)
+    if cone:  # ClassicalMPCConfig defaults (crocoddyl_classical.py:59-61)
+        c.w_friction_cone, c.mu = 2.0e2, 0.6
+    return c
+
+
+@pytest.mark.parametrize("variant,contact,surf,cone", CASES)
+def test_calc_diff_matches_oracle(variant, contact, surf, cone):
     N, B = 4, 3
-    cfg = product_cfg(variant, N, contact)
+    cfg = _cfg(variant, N, contact, cone)
     ocfg = oracle_cfg(cfg)
     b = make_batch(variant, B, N, seed=11 + surf, surface=surf)
     rng = np.random.default_rng(7)
@@ -43,78 +73,129 @@ def test_calc_diff_matches_oracle(variant, contact, surf):
     us = b.us_init + 0.5 * rng.normal(size=b.us_init.shape)
     solver = BatchedBoxFDDP(cfg, max_batch=B)
     out = solver.calc_diff(b, xs, us)
+    worst = {}
     for i in range(B):
         prob = oracle_problem(b, i, N)
         run = ocp.running_eval(ocfg, prob, slice(0, N), xs[i, :N], us[i], True)
         term = ocp.terminal_eval(ocfg, prob, xs[i, N], True)
-        for key in ("Fx", "Fu", "Lx", "Lu", "Lxx", "Lxu", "Luu"):
-            assert rel_err(out[key][i, :N], run[key]) < TOL_NODE, (key, rel_err(out[key][i, :N], run[key]))
-        assert rel_err(out["cost"][i, :N], run["cost"]) < TOL_NODE
-        assert rel_err(out["xnext"][i], run["xnext"]) < TOL_NODE
-        assert rel_err(out["Lx"][i, N], term["Lx"]) < TOL_NODE
-        assert rel_err(out["Lxx"][i, N], term["Lxx"]) < TOL_NODE
-        assert rel_err(out["cost"][i, N], term["cost"]) < TOL_NODE
+        errs = {k: rel_err(out[k][i, :N], run[k]) for k in ("Fx", "Fu", "Lx", "Lu", "Lxx", "Lxu", "Luu", "cost", "xnext")}
+        errs["Lx_T"] = rel_err(out["Lx"][i, N], term["Lx"])
+        errs["Lxx_T"] = rel_err(out["Lxx"][i, N], term["Lxx"])
+        errs["cost_T"] = rel_err(out["cost"][i, N], term["cost"])
         if surf:
-            nc = ocfg.nc
-            assert rel_err(out["lam"][i, :N, :nc], run["lam"]) < TOL_NODE
+            errs["lam"] = rel_err(out["lam"][i, :N, :ocfg.nc], run["lam"])
+        for k, e in errs.items():
+            worst[k] = max(worst.get(k, 0.0), e)
+    log_parity(f"calc_diff/{variant}/{contact}/surf{surf}/cone{cone}", **worst)
+    for k, e in worst.items():
+        assert e < TOL_NODE, (k, e)
 
 
-@pytest.mark.parametrize("variant,contact,surf", CASES)
-def test_solve_matches_oracle(variant, contact, surf):
+def _check_solves(name, cfg, b, solver, ref, tol=TOL_SOLVE, tol_k=TOL_K):
+    """Identical discrete path and close continuous outputs; logs the errors."""
+    e = dict(xs=0.0, us=0.0, K=0.0, cost=0.0)
+    for i, r in enumerate(ref):
+        assert bool(solver.ok[i]) == r["ok"], (i, solver.ok[i], r["ok"])
+        assert int(solver.iter[i]) == r["iter"], (i, solver.iter[i], r["iter"])
+        st = solver.stats[i]
+        assert int(st[2]) == r["reg_retries"], (i, "retries", st[2], r["reg_retries"])
+        assert int(st[0]) == r["iters_run"] - r["reg_retries"], (i, "iters", st[0], r["iters_run"])
+        assert int(st[1]) == r["trials"], (i, "trials", st[1], r["trials"])
+        e["xs"] = max(e["xs"], rel_err(solver.xs[i], r["xs"]))
+        e["us"] = max(e["us"], rel_err(solver.us[i], r["us"]))
+        e["K"] = max(e["K"], rel_err(solver.K[i], r["K"]))
+        e["cost"] = max(e["cost"], rel_err(solver.cost[i], r["cost"]))
+    totals = {k: int(sum(r[k] for r in ref)) for k in ("reg_retries", "forward_errors", "neg_branch", "clamped")}
+    log_parity(name, B=len(ref), **e, **totals)
+    assert e["xs"] < tol and e["us"] < tol and e["cost"] < tol, e
+    assert e["K"] < tol_k, e
+    return totals
+
+
+@pytest.mark.parametrize("variant,contact,surf,cone", CASES)
+def test_solve_matches_oracle(variant, contact, surf, cone):
     N = 30 if contact == "normal_1d" else 12
     B = 4
-    cfg = product_cfg(variant, N, contact)
+    cfg = _cfg(variant, N, contact, cone)
     b = make_batch(variant, B, N, seed=21 + surf, surface=surf)
     solver = BatchedBoxFDDP(cfg, max_batch=B)
-    ok = solver.solve(b, maxiter=10, is_feasible=False)
-    for i in range(B):
-        ok_o, s = oracle_solve(cfg, b, i)
-        assert bool(ok[i]) == bool(ok_o)
-        assert int(solver.iter[i]) == int(s.iter), (i, solver.iter[i], s.iter)
-        assert rel_err(solver.cost[i], s.cost) < TOL_SOLVE
-        assert rel_err(solver.xs[i], s.xs) < TOL_SOLVE
-        assert rel_err(solver.us[i], s.us) < TOL_SOLVE
-        assert rel_err(solver.K[i], s.K) < TOL_SOLVE * 10
-        assert int(solver.stats[i, 0]) == s.stats.iters_run - s.stats.reg_retries or s.stats.reg_retries > 0
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B))
+    tol, tol_k = CASE_TOL.get((variant, contact, surf, cone), (TOL_SOLVE, TOL_K))
+    _check_solves(f"solve/{variant}/{contact}/surf{surf}/cone{cone}", cfg, b, solver, ref, tol, tol_k)
 
 
-def test_gravity_torque_dev_matches_oracle():
-    import torch
-    from ffddp import _abi
-    from oracle import panda as P
-
-    cfg = product_cfg("classical", 4)
-    solver = BatchedBoxFDDP(cfg, max_batch=8)
-    rng = np.random.default_rng(3)
-    q = P.Q_NEUTRAL + rng.uniform(-0.5, 0.5, size=(64, 7))
-    qd = torch.tensor(q, device="cuda")
-    td = torch.zeros_like(qd)
-    import ctypes
-
-    rc = solver._lib.ffddp_gravity_torque_dev(solver._h, 64, ctypes.c_void_p(qd.data_ptr()), ctypes.c_void_p(td.data_ptr()), None)
-    assert rc == 0
-    torch.cuda.synchronize()
-    assert rel_err(td.cpu().numpy(), P.gravity_torque(q)) < 1e-12
+def test_solve_random_regime_horizon30():
+    """BASELINE configs[1] shape: the SURVEY-literal random x0 (q_neutral +
+    U(+-0.15), v ~ N(0, 0.1^2)) at N = 30, 32 instances."""
+    N, B = 30, 32
+    cfg = product_cfg("classical", N)
+    b = make_batch("classical", B, N, seed=101, regime="random")
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B))
+    _check_solves("solve/random/N30/B32", cfg, b, solver, ref, tol=2e-7, tol_k=4e-8)
 
 
-@pytest.mark.parametrize("box,regime", [(False, "tracking"), (True, "random")])
-def test_solve_variants_match_oracle(box, regime):
-    """Plain FDDP (use_box_fddp=False: Cholesky gains, no clamping, th_stop 1e-9)
-    and the SURVEY-literal random x0 regime."""
+def test_solve_plain_fddp():
+    """use_box_fddp = False (SolverFDDP: Cholesky gains, no clamping, th_stop 1e-9)."""
     N, B = 20, 4
     cfg = product_cfg("classical", N)
-    cfg.use_box_fddp = box
-    b = make_batch("classical", B, N, seed=33, surface=1, regime=regime)
+    cfg.use_box_fddp = False
+    b = make_batch("classical", B, N, seed=33, surface=1)
     solver = BatchedBoxFDDP(cfg, max_batch=B)
-    ok = solver.solve(b, maxiter=10, is_feasible=False)
-    for i in range(B):
-        ok_o, s = oracle_solve(cfg, b, i, box=box)
-        assert bool(ok[i]) == bool(ok_o)
-        assert int(solver.iter[i]) == int(s.iter), (i, solver.iter[i], s.iter)
-        assert rel_err(solver.cost[i], s.cost) < TOL_SOLVE
-        assert rel_err(solver.xs[i], s.xs) < TOL_SOLVE
-        assert rel_err(solver.us[i], s.us) < TOL_SOLVE
-        assert rel_err(solver.K[i], s.K) < TOL_SOLVE * 10
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B), box=False)
+    _check_solves("solve/plain_fddp", cfg, b, solver, ref)
+
+
+def test_solve_boxqp_active_bounds():
+    """Tight torque limits: the feasible iterations' BoxQP has clamped controls
+    (K = Quu_ff^-1 Qxu_f^T on the free set, Qu[clamped] = 0)."""
+    N, B = 12, 4
+    cfg = product_cfg("classical", N)
+    cfg.tau_limits = np.array([20.0, 20, 20, 20, 3, 3, 3])
+    b = make_batch("classical", B, N, seed=21, surface=1)
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B))
+    assert all(r["clamped"] > 0 for r in ref)
+    assert np.all(np.abs(solver.us) <= cfg.tau_limits + 1e-12)
+    assert np.any(np.abs(np.abs(solver.us) - cfg.tau_limits) < 1e-12)  # controls sit on the bounds
+    _check_solves("solve/boxqp_clamped", cfg, b, solver, ref)
+
+
+def test_solve_backward_failures_retry():
+    """A negative torque-regularisation weight makes Quu indefinite at the
+    minimum regularisation: the backward pass fails, preg grows x10 and the
+    pass is retried (SolverFDDP::solve / computeDirection)."""
+    N, B = 12, 4
+    cfg = product_cfg("classical", N)
+    cfg.w_tau = -0.05
+    b = make_batch("classical", B, N, seed=21, surface=1)
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B))
+    assert all(r["reg_retries"] > 0 for r in ref)
+    assert np.all(solver.stats[:, 2] > 0)
+    _check_solves("solve/backward_retries", cfg, b, solver, ref)
+
+
+def test_solve_nonfinite_line_search_trials():
+    """x0 with a 50 rad/s velocity offset and an xs_init[0] that does not
+    contain it: the alpha = 1 rollout starts at x0 and overflows (raiseIfNaN:
+    the trial is rejected), shorter steps stay finite."""
+    N, B = 12, 4
+    cfg = product_cfg("classical", N)
+    b = make_batch("classical", B, N, seed=21, surface=1)
+    b.x0 = b.x0.copy()
+    b.x0[:, 7:] += 50.0
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B))
+    assert all(r["forward_errors"] > 0 for r in ref)
+    totals = _check_solves("solve/nonfinite_trials", cfg, b, solver, ref, tol=1.5e-9, tol_k=TOL_K)
+    assert totals["neg_branch"] > 0
 
 
 def test_long_horizon_point3d_matches_oracle():
@@ -123,12 +204,27 @@ def test_long_horizon_point3d_matches_oracle():
     cfg = product_cfg("classical", N, "point3d")
     b = make_batch("classical", B, N, seed=55, surface=1)
     solver = BatchedBoxFDDP(cfg, max_batch=B)
-    ok = solver.solve(b, maxiter=10, is_feasible=False)
-    for i in range(B):
-        ok_o, s = oracle_solve(cfg, b, i)
-        assert bool(ok[i]) == bool(ok_o)
-        assert int(solver.iter[i]) == int(s.iter), (i, solver.iter[i], s.iter)
-        assert rel_err(solver.cost[i], s.cost) < TOL_SOLVE
-        assert rel_err(solver.xs[i], s.xs) < TOL_SOLVE
-        assert rel_err(solver.us[i], s.us) < TOL_SOLVE
-        assert rel_err(solver.K[i], s.K) < TOL_SOLVE * 10
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B))
+    _check_solves("solve/point3d/N100", cfg, b, solver, ref, tol=6e-7, tol_k=2e-6)
+
+
+def test_gravity_torque_dev_matches_oracle():
+    import ctypes
+
+    import torch
+    from oracle import panda as P
+
+    cfg = product_cfg("classical", 4)
+    solver = BatchedBoxFDDP(cfg, max_batch=8)
+    rng = np.random.default_rng(3)
+    q = P.Q_NEUTRAL + rng.uniform(-0.5, 0.5, size=(64, 7))
+    qd = torch.tensor(q, device="cuda")
+    td = torch.zeros_like(qd)
+    rc = solver._lib.ffddp_gravity_torque_dev(solver._h, 64, ctypes.c_void_p(qd.data_ptr()),
+                                              ctypes.c_void_p(td.data_ptr()), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    err = rel_err(td.cpu().numpy(), P.gravity_torque(q))
+    log_parity("gravity_dev", err=err)
+    assert err < 1e-12

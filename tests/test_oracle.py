@@ -101,19 +101,33 @@ def test_contact_kkt_residuals():
     assert np.allclose(Jc @ d["a"] + gam, -cfg.contact_inv_damping * lam, atol=1e-9)
 
 
-CASES = [(v, c, s) for v in ("classical", "ff") for c in ("normal_1d", "point3d") for s in (0, 1)]
+CASES = [(v, c, s, 0) for v in ("classical", "ff") for c in ("normal_1d", "point3d") for s in (0, 1)]
+# point3d with the friction cone on (ClassicalMPCConfig defaults w = 2e2, mu = 0.6)
+CASES += [("classical", "point3d", 1, 1), ("ff", "point3d", 1, 1)]
 
 
-@pytest.mark.parametrize("variant,contact,surf", CASES)
-def test_node_derivatives_finite_differences(variant, contact, surf):
+def cone_cfg(variant, N, contact="point3d"):
+    c = product_cfg(variant, N, contact)
+    c.w_friction_cone, c.mu = 2.0e2, 0.6
+    return c
+
+
+@pytest.mark.parametrize("variant,contact,surf,cone", CASES)
+def test_node_derivatives_finite_differences(variant, contact, surf, cone):
     N = 3
-    cfg = oracle_cfg(product_cfg(variant, N, contact))
+    cfg = oracle_cfg(cone_cfg(variant, N, contact) if cone else product_cfg(variant, N, contact))
     b = make_batch(variant, 1, N, seed=4, surface=surf)
     prob = oracle_problem(b, 0, N)
     rng = np.random.default_rng(9)
     nx = cfg.nx
     x = b.x0[0] + 0.03 * rng.normal(size=nx)
     u = b.us_init[0, 0] + 0.3 * rng.normal(size=7)
+    if cone:
+        # the cone's facet rows must be active at this point for the test to bite
+        lam = ocp.running_eval(cfg, prob, 1, x, u, False)["lam"]
+        A, lb, ub = ocp.friction_cone(cfg)
+        r = A @ lam
+        assert np.any(r > ub) or np.any(r < lb), (lam, r)
     d = ocp.running_eval(cfg, prob, 1, x, u, True)
     h = 1e-6
 
@@ -259,3 +273,20 @@ def test_backward_failure_raises_regularisation():
     s = fddp.SolverBoxFDDP(m, box=False)
     s.solve(np.zeros((m.N + 1, m.nx)), np.zeros((m.N, m.nu)), maxiter=3)
     assert s.stats.reg_retries > 0
+
+
+def test_accept_step_rule():
+    """SolverFDDP::solve acceptance (oracle.fddp.accept_step, the rule the HIP
+    kernel's trial_accepted implements)."""
+    c = fddp.Consts()
+    # descent direction: sufficient decrease
+    assert fddp.accept_step(c, False, dV=0.2, d0=1.0, dVexp=1.0)
+    assert not fddp.accept_step(c, False, dV=0.05, d0=1.0, dVexp=1.0)
+    assert fddp.accept_step(c, True, dV=-1.0, d0=1e-13, dVexp=1e-13)  # |d0| < th_grad
+    # ascent direction while infeasible: a rise of up to 2x the predicted one
+    assert fddp.accept_step(c, False, dV=-1.5, d0=-1.0, dVexp=-1.0)
+    assert not fddp.accept_step(c, False, dV=-2.5, d0=-1.0, dVexp=-1.0)
+    # ascent direction once feasible: never (Crocoddyl 2.x `!is_feasible_ && ...`),
+    # even for a trial that lowers the cost
+    assert not fddp.accept_step(c, True, dV=-0.5, d0=-1.0, dVexp=-1.0)
+    assert not fddp.accept_step(c, True, dV=+0.5, d0=-1.0, dVexp=-1.0)
