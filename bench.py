@@ -3,18 +3,25 @@
 
 BASELINE.json metric: "FDDP solves/sec, Franka 7-DoF horizon-30 batch=4096,
 at 1/2/4/8 MI355X".  One step = one solver.solve(xs_init, us_init, 10, False)
-(crocoddyl_classical.py:367) for a batch of B synthetic OCP instances per GPU
-(classical nx=14 nu=7, contact model normal_1d, cold warm start), inputs
-already resident in HBM.  N GPUs = N independent shards (one process per GPU,
-weak scaling); the only collective is the final all-gather of per-instance
-costs and first controls (RCCL, the exchange the north star names).
+(crocoddyl_classical.py:367) of every instance of ONE global batch of B = 4096
+synthetic OCP instances (classical nx=14 nu=7, contact model normal_1d, cold
+warm start), inputs already resident in HBM.  G GPUs split the global batch
+into contiguous slices (one process per GPU, strong scaling, SURVEY.md §8(e));
+the only collective is the final all-gather of the per-instance results over
+RCCL ("costs": cost, iters, ok, u0 by default; "full": xs, us, K, cost).
 
 Prints ONE JSON line (rank 0).  Extra objects:
-  roofline      dominant kernel's algorithmic bytes per launch / its average
-                HIP-event-timed launch duration, vs 8 TB/s.
-  cpu_baseline  the numpy oracle (oracle/, the CPU restatement) timed on a
-                bounded sample of the same workload on the host cores (one
-                worker process per core, up to 16), in a child process.
+  roofline      SURVEY §8(d): algorithmic HBM bytes of the whole solve (every
+                kernel, from the device-counted iterations / line-search
+                trials) / wall time of the timed region, vs 8 TB/s; plus the
+                per-kernel fractions from a separate single-stream profiling
+                step (HIP events around every launch, no overlap) and the
+                PMC-measured traffic when profiles/ holds it for this config.
+  cpu_baseline  the C++ scalar BoxFDDP (oracle/cpu, the same OCP and solver
+                algorithm) on the host cores, OpenMP over the same instances.
+  weak          (G > 1) every rank solving its own 4096-instance batch.
+  random_regime the SURVEY-literal x0 draw (q_neutral + U(+-0.15)), same B.
+  host_io       PCIe-inclusive rate of the host-array entry point.
 """
 from __future__ import annotations
 
@@ -34,13 +41,16 @@ import numpy as np  # noqa: E402
 METRIC = "FDDP solves/sec, Franka 7-DoF horizon-30 batch=4096, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0  # float4 copy, same table
-FP64_VALU_PEAK_TFLOPS = 78.6  # AMD public MI355X vector fp64 spec
+SEED = 1234
 
 
 def algorithmic_words(nx: int, nu: int, N: int):
     """Per-node fp64 words of the staged calcDiff -> backward -> forward design
     (SURVEY.md §8(d)): A = calcDiff (running node), B = backward, C = one
-    forward trial; *_T the terminal node; IO per solve."""
+    forward trial (SURVEY's per-trial count); *_T the terminal node; IO per
+    solve.  The line search reads (xs, us, K, k, fs, w, refs) once per
+    instance per launch however many step lengths it evaluates concurrently
+    (C_shared) and writes one trial per step length (C_trial)."""
     a_r = 2 * nx + nu + 6
     a_w = 2 * nx * nx + 2 * nx * nu + nu * nu + 2 * nx + nu + 1
     A = a_r + a_w
@@ -50,131 +60,107 @@ def algorithmic_words(nx: int, nu: int, N: int):
     B_T = nx * nx + 2 * nx
     C_T = 4 * nx + 6
     io = nx + (N + 1) * nx + N * nu + (N + 1) * 6 + 21 + (N + 1) * nx + N * nu + N * nu * nx + 1
-    return dict(A=A, B=Bw, C=Cf, A_T=A_T, B_T=B_T, C_T=C_T, IO=io)
+    C_shared = N * (3 * nx + 2 * nu + nu * nx + 6) + (3 * nx + 6)
+    C_trial = N * (nx + nu) + nx
+    return dict(A=A, B=Bw, C=Cf, A_T=A_T, B_T=B_T, C_T=C_T, IO=io, C_shared=C_shared, C_trial=C_trial,
+                primal=2 * nx + nu + 6 + nx + 1)
 
 
-def kernel_bytes(stats: np.ndarray, nx: int, nu: int, N: int) -> dict:
-    """Algorithmic bytes of one solve of the whole batch, per kernel class
-    (one kernel per class): node = the calcDiff record (A words per running
-    node), primal = the calc's reads (x_t, u_t, x_t+1, refs) and writes (gap,
-    cost), backward = B words per node, forward / forward2 = C words per node
-    for every step length the first / second line-search pass evaluated."""
+def solve_bytes(stats: np.ndarray, nx: int, nu: int, N: int) -> dict:
+    """Algorithmic bytes of one batched solve, per kernel class and in total,
+    from the per-instance device counters (include/ffddp.h stats):
+    [0] successful backward passes (= first-pass line-search launches),
+    [4] calcDiffs, [5] line-search launches (both passes), [6]/[7] step
+    lengths evaluated by the first / second pass."""
     w = algorithmic_words(nx, nu, N)
-    n_calc = stats[:, 4].astype(np.float64)
-    n_bw = stats[:, 0].astype(np.float64)
-    ev1 = stats[:, 6].astype(np.float64)
-    ev2 = stats[:, 7].astype(np.float64)
-    primal_words = 2 * nx + nu + 6 + nx + 1
-    per_trial = N * w["C"] + w["C_T"]
-    return {
-        "node": 8.0 * float(np.sum(n_calc)) * (N * w["A"] + w["A_T"]),
-        "primal": 8.0 * float(np.sum(n_calc)) * (N + 1) * primal_words,
-        "backward": 8.0 * float(np.sum(n_bw)) * (N * w["B"] + w["B_T"]),
-        "forward": 8.0 * float(np.sum(ev1)) * per_trial,
-        "forward2": 8.0 * float(np.sum(ev2)) * per_trial,
+    s = stats.astype(np.float64)
+    n_calc, n_bw, n_fw, ev1, ev2 = s[:, 4].sum(), s[:, 0].sum(), s[:, 5].sum(), s[:, 6].sum(), s[:, 7].sum()
+    calc = 8.0 * n_calc * (N * w["A"] + w["A_T"])
+    primal = 8.0 * n_calc * (N + 1) * w["primal"]
+    out = {
+        "primal": primal,
+        "node": calc - primal,
+        "backward": 8.0 * n_bw * (N * w["B"] + w["B_T"]),
+        "forward": 8.0 * (n_bw * w["C_shared"] + ev1 * w["C_trial"]),
+        "forward2": 8.0 * ((n_fw - n_bw) * w["C_shared"] + ev2 * w["C_trial"]),
         "io": 8.0 * stats.shape[0] * w["IO"],
     }
+    out["total"] = out["primal"] + out["node"] + out["backward"] + out["forward"] + out["forward2"] + out["io"]
+    # SURVEY §8(d) literal: every evaluated step length reads its inputs again
+    out["total_survey_formula"] = 8.0 * (n_calc * (N * w["A"] + w["A_T"]) + n_bw * (N * w["B"] + w["B_T"]) +
+                                         (ev1 + ev2) * (N * w["C"] + w["C_T"]) + stats.shape[0] * w["IO"])
+    return out
 
 
-def _oracle_solve_one(args):
-    """Worker: one oracle solve of instance i (CPU restatement, maxiter=10)."""
-    cfg_kw, i = args
-    from oracle import fddp, ocp  # noqa: WPS433 (checker import, baseline leg only)
+def pmc_traffic(variant, contact, B, N):
+    """Per-solve HBM bytes per kernel class measured by rocprofv3 PMC passes
+    (tools/pmc_traffic.py -> profiles/traffic_latest.json), if they are for
+    this configuration."""
+    tf = ROOT / "profiles" / "traffic_latest.json"
+    if not tf.exists():
+        return None
+    try:
+        tj = json.loads(tf.read_text())
+    except ValueError:
+        return None
+    if tj.get("config") != f"{variant}/{contact}/B{B}/N{N}":
+        return None
+    return {k: v.get("hbm_bytes_per_solve") for k, v in tj.get("kernels", {}).items()}
 
-    batch = _CPU_STATE["batch"]
-    prob = ocp.Problem(batch.x0[i], batch.node_ref[i, :, :3], batch.node_ref[i, :, 3:], batch.inst_ref[i, :14],
-                       batch.inst_ref[i, 14:], bool(batch.surface[i]))
-    s = fddp.SolverBoxFDDP(_CPU_STATE["ocfg"], prob)
-    s.solve(batch.xs_init[i], batch.us_init[i], 10, False)
-    return i
 
+def cpu_baseline(cfg, batch, maxiter: int, budget_s: float) -> dict:
+    """The C++ scalar BoxFDDP (oracle/cpu) on the host cores: OpenMP over the
+    same instances, one per thread at a time; warm-up, then the median of 3
+    timed runs over the batch (bounded to about budget_s of CPU work)."""
+    from ffddp import _abi
+    from oracle import cpu_fddp  # checker / baseline leg only
 
-_CPU_STATE: dict = {}
-
-
-def _cpu_worker(argv) -> None:
-    """Child process of the cpu_baseline leg (never touches the GPU): rebuilds
-    the same seeded batch, times the oracle over a bounded sample on all the
-    host cores this process may use, prints one JSON object."""
-    import multiprocessing as mp
-
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int)
-    ap.add_argument("--horizon", type=int)
-    ap.add_argument("--variant")
-    ap.add_argument("--contact")
-    ap.add_argument("--regime")
-    ap.add_argument("--seed", type=int)
-    ap.add_argument("--budget", type=float)
-    a = ap.parse_args(argv)
-    from ffddp import _abi, robot as R, workload
-    from ffddp.config import classical_preset, ff_preset
-
-    sys.path.insert(0, str(ROOT / "tests"))
-    from helpers import oracle_cfg  # noqa: E402
-
-    cfg = ff_preset(a.horizon, a.contact) if a.variant == "ff" else classical_preset(a.horizon, a.contact)
-    ee = R.R_MJ_FROM_PIN @ _abi.frame_placement(R.Q_NEUTRAL)[1]
-    batch = workload.make_batch(a.batch, a.horizon, a.variant, _abi.gravity_torque, ee, seed=a.seed,
-                                regime=a.regime, fk=_abi.frame_placement)
-    _CPU_STATE["batch"] = batch
-    _CPU_STATE["ocfg"] = oracle_cfg(cfg)
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    workers = max(1, min(16, cores))  # the GPU box grants 16 CPUs per GPU
+    threads = max(1, min(16, cores))  # the GPU box grants 16 CPUs per GPU
+    rb, cs = _abi.robot_struct(), cfg.to_struct()
+    warm = batch.slice(slice(0, min(batch.B, 2 * threads)))
     t0 = time.perf_counter()
-    _oracle_solve_one((None, 0))
-    t1 = time.perf_counter() - t0
-    n = int(min(batch.B, max(workers, workers * max(1, int(a.budget / max(t1, 1e-3))))))
-    ctx = mp.get_context("fork")
-    t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
-        pool.map(_oracle_solve_one, [(None, i) for i in range(n)], chunksize=1)
-    dt = time.perf_counter() - t0
-    print(json.dumps({
-        "value": n / dt, "unit": "solves/s", "cores": workers, "kind": "port",
-        "sample": f"first {n} instances of the rank-0 batch (same seed/workload), numpy oracle (oracle/fddp.py), "
-                  f"maxiter=10, {workers} worker processes, {dt:.1f} s wall ({t1:.2f} s for one solve on one core)",
-    }))
-
-
-def cpu_baseline(args, seed: int) -> dict:
-    """The oracle timed on the host cores in a child process (the GPU is
-    initialised in this one); bounded to about args.cpu_budget seconds."""
-    import subprocess
-
-    cmd = [sys.executable, str(Path(__file__).resolve()), "--_cpu_worker", "--batch", str(args.batch), "--horizon",
-           str(args.horizon), "--variant", args.variant, "--contact", args.contact, "--regime", args.regime, "--seed",
-           str(seed), "--budget", str(args.cpu_budget)]
-    # one BLAS thread per worker process: the oracle's matrices are tiny and
-    # the workers already cover the cores
-    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=max(120.0, 10 * args.cpu_budget), env=env)
-    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
-    if r.returncode != 0 or not lines:
-        return {"value": None, "error": (r.stderr or r.stdout)[-400:]}
-    return json.loads(lines[-1])
+    cpu_fddp.solve_batch(rb, cs, warm, maxiter=maxiter, nthreads=threads)
+    per_solve = (time.perf_counter() - t0) / warm.B * threads
+    n = int(min(batch.B, max(2 * threads, budget_s / 3.0 / max(per_solve, 1e-6) * threads)))
+    sample = batch.slice(slice(0, n))
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        out = cpu_fddp.solve_batch(rb, cs, sample, maxiter=maxiter, nthreads=threads)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {
+        "value": n / med, "unit": "solves/s", "cores": threads, "kind": "port",
+        "sample": f"first {n} of the {batch.B} instances of the same seeded workload; C++ scalar BoxFDDP "
+                  f"(oracle/cpu/ffddp_cpu.cpp: the product's node models compiled for the host + a sequential "
+                  f"Crocoddyl-style solver), OpenMP {threads} threads, maxiter={maxiter}, median of 3 runs "
+                  f"({med:.2f} s each; ok {float(np.mean(out['ok'])):.2f}, mean iter {float(np.mean(out['iter'])):.2f})",
+    }
 
 
 def main():
-    if len(sys.argv) > 1 and sys.argv[1] == "--_cpu_worker":
-        return _cpu_worker(sys.argv[2:])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--batch", type=int, default=4096, help="global batch, split over the GPUs")
     ap.add_argument("--horizon", type=int, default=30)
     ap.add_argument("--variant", choices=("classical", "ff"), default="classical")
     ap.add_argument("--contact", choices=("normal_1d", "point3d"), default="normal_1d")
     ap.add_argument("--maxiter", type=int, default=10)
     ap.add_argument("--regime", choices=("tracking", "random"), default="tracking")
+    ap.add_argument("--gather", choices=("costs", "full", "none"), default="costs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP-event timing")
-    ap.add_argument("--no-host-io", action="store_true", help="skip the PCIe-inclusive host-array rate")
+    ap.add_argument("--no-profile", action="store_true", help="skip the single-stream per-kernel profiling step")
+    ap.add_argument("--profile-only", action="store_true",
+                    help="run only the single-stream profiling step (for rocprofv3 of the per-kernel numbers)")
+    ap.add_argument("--no-host-io", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the weak-scaling and random-regime extras")
     args = ap.parse_args()
 
     import torch
@@ -188,118 +174,182 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
-    B, N = args.batch, args.horizon
+    B, N, nu = args.batch, args.horizon, 7
     cfg = ff_preset(N, args.contact) if args.variant == "ff" else classical_preset(N, args.contact)
-    nx, nu = cfg.nx, 7
+    nx = cfg.nx
     ee = R.R_MJ_FROM_PIN @ _abi.frame_placement(R.Q_NEUTRAL)[1]
-    batch = workload.make_batch(
-        B, N, args.variant, _abi.gravity_torque, ee, seed=shard.shard_seed(1234, rank), regime=args.regime,
-        fk=_abi.frame_placement,
-    )
+
+    def make(Bg, seed, regime):
+        return workload.make_batch(Bg, N, args.variant, _abi.gravity_torque, ee, seed=seed, regime=regime,
+                                   fk=_abi.frame_placement)
+
     f64 = dict(dtype=torch.float64, device=dev)
-    T = dict(
-        x0=torch.tensor(batch.x0, **f64),
-        node_ref=torch.tensor(batch.node_ref, **f64),
-        inst_ref=torch.tensor(batch.inst_ref, **f64),
-        surface=torch.tensor(batch.surface, dtype=torch.uint8, device=dev),
-        xs_init=torch.tensor(batch.xs_init, **f64),
-        us_init=torch.tensor(batch.us_init, **f64),
-        xs=torch.zeros((B, N + 1, nx), **f64),
-        us=torch.zeros((B, N, nu), **f64),
-        K=torch.zeros((B, N, nu, nx), **f64),
-        cost=torch.zeros(B, **f64),
-        iters=torch.zeros(B, dtype=torch.int32, device=dev),
-        ok=torch.zeros(B, dtype=torch.uint8, device=dev),
-        fn_pred=torch.zeros((B, 2), **f64),
-        stats=torch.zeros((B, _abi.NSTATS), dtype=torch.int32, device=dev),
-    )
-    solver = BatchedBoxFDDP(cfg, max_batch=B, device=local_rank)
+
+    def tensors(b):
+        Bl = b.B
+        return dict(
+            x0=torch.tensor(b.x0, **f64), node_ref=torch.tensor(b.node_ref, **f64),
+            inst_ref=torch.tensor(b.inst_ref, **f64),
+            surface=torch.tensor(b.surface, dtype=torch.uint8, device=dev),
+            xs_init=torch.tensor(b.xs_init, **f64), us_init=torch.tensor(b.us_init, **f64),
+            xs=torch.zeros((Bl, N + 1, nx), **f64), us=torch.zeros((Bl, N, nu), **f64),
+            K=torch.zeros((Bl, N, nu, nx), **f64), cost=torch.zeros(Bl, **f64),
+            iters=torch.zeros(Bl, dtype=torch.int32, device=dev), ok=torch.zeros(Bl, dtype=torch.uint8, device=dev),
+            fn_pred=torch.zeros((Bl, 2), **f64),
+            stats=torch.zeros((Bl, _abi.NSTATS), dtype=torch.int32, device=dev),
+        )
+
     stream = torch.cuda.current_stream(dev).cuda_stream
-    gathered = torch.zeros((world, B, 1 + nu), **f64) if world > 1 else None
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+
+    # ---- the metric: one global batch, contiguous slice per rank ----
+    glob = make(B, SEED, args.regime)
+    b0, b1 = shard.slice_bounds(B, world, rank)
+    mine = glob.slice(slice(b0, b1))
+    T = tensors(mine)
+    counts = shard.slice_counts(B, world)
+    solver = BatchedBoxFDDP(cfg, max_batch=max(counts), device=local_rank)
+    gather = None
+    if world > 1 and args.gather != "none":
+        width = shard.pack_results(T, args.gather).shape[1]
+        gather = shard.Gatherer(counts, width, dev)
 
     def step():
         solver.solve_dev(T, maxiter=args.maxiter, is_feasible=False, stream=stream)
-        if world > 1:  # final exchange: per-instance cost + first control to every rank
-            shard.gather_results(T["cost"], T["us"][:, 0, :], gathered)
+        if gather is not None:
+            gather(shard.pack_results(T, args.gather))
 
-    # warmup; the last warmup step times every kernel class once to find the
-    # dominant kernel, and only that kernel is event-timed inside the timed
-    # region (events around every launch of 3 streams would perturb it)
-    warm_prof = None
-    for w in range(args.warmup):
-        if not args.no_profile and w == args.warmup - 1:
-            solver.profile(True)
-            solver.profile_read(reset=True)
-        step()
-    torch.cuda.synchronize(dev)
-    dom = None
-    if not args.no_profile:
-        warm_prof = solver.profile_read(reset=True)
-        dom = max(("primal", "node", "backward", "forward"), key=lambda k: warm_prof[k][0])
-        solver.profile([dom])
-        solver.profile_read(reset=True)
-    elapsed = shard.timed_steps(step, args.steps, lambda: torch.cuda.synchronize(dev))
-    prof = solver.profile_read(reset=True) if not args.no_profile else None
+    elapsed = None
+    if not args.profile_only:
+        for _ in range(args.warmup):
+            step()
+        sync()
+        elapsed = shard.timed_steps(step, args.steps, sync)
 
     stats = T["stats"].cpu().numpy()
     ok = T["ok"].cpu().numpy()
     iters = T["iters"].cpu().numpy()
     cost = T["cost"].cpu().numpy()
-    total = B * world * args.steps
-    value = total / elapsed
+    sb = solve_bytes(stats, nx, nu, N)
+    # whole-job sums over ranks: algorithmic bytes per step, ok count, iterations
+    tot = shard.sum_over_ranks(torch.tensor([sb["total"], sb["total_survey_formula"], float(ok.sum()),
+                                             float(iters.sum())], **f64)).cpu().numpy()
+    tot_bytes, tot_survey, tot_ok, tot_it = (float(v) for v in tot)
 
-    roofline = None
-    kernels = None
-    if prof is not None:
-        kb = kernel_bytes(stats, nx, nu, N)
-        # per-class times of the (untimed) profiling warmup step, for reference
-        kernels = {k: {"ms_per_solve": v[0], "launches_per_solve": v[1]} for k, v in warm_prof.items() if v[1] > 0}
-        ms, launches = prof[dom]
-        avg_launch_s = ms / 1e3 / max(1, launches)
-        bytes_per_launch = kb[dom] * args.steps / max(1, launches)
-        achieved = bytes_per_launch / avg_launch_s / 1e9
-        traffic = None
-        tf = ROOT / "profiles" / "traffic_latest.json"
-        if tf.exists():
-            try:
-                tj = json.loads(tf.read_text())
-                if tj.get("config") == f"{args.variant}/{args.contact}/B{B}/N{N}":
-                    per_solve = tj.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_solve")
-                    if per_solve is not None:
-                        traffic = per_solve * args.steps / max(1, launches)
-            except Exception:
-                traffic = None
-        roofline = {
-            "bound": "hbm",
-            "kernel": dom,
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "bytes_per_launch": bytes_per_launch,
-            "avg_launch_ms": avg_launch_s * 1e3,
-            "frac_of_measured_copy": achieved / HBM_MEASURED_GBS,
-        }
+    # ---- per-kernel profiling: the same slice on ONE stream, HIP events
+    # around every launch (no overlap between launches) ----
+    kernels = dominant = None
+    if not args.no_profile:
+        old = os.environ.get("FFDDP_STREAMS")
+        os.environ["FFDDP_STREAMS"] = "1"
+        psolver = BatchedBoxFDDP(cfg, max_batch=max(counts), device=local_rank)
+        if old is None:
+            del os.environ["FFDDP_STREAMS"]
+        else:
+            os.environ["FFDDP_STREAMS"] = old
+        psolver.solve_dev(T, maxiter=args.maxiter, stream=stream)  # warm-up
+        sync()
+        psolver.profile(True)
+        psolver.profile_read(reset=True)
+        n_prof = 2
+        t0 = time.perf_counter()
+        for _ in range(n_prof):
+            psolver.solve_dev(T, maxiter=args.maxiter, stream=stream)
+        sync()
+        t_single = (time.perf_counter() - t0) / n_prof
+        prof = psolver.profile_read(reset=True)
+        psolver.profile(False)
+        pstats = T["stats"].cpu().numpy()
+        pb = solve_bytes(pstats, nx, nu, N)
+        total_ms = sum(v[0] for v in prof.values())
+        kernels = {}
+        for k, (ms, n) in prof.items():
+            if n == 0:
+                continue
+            e = {"ms_per_solve": ms / n_prof, "launches_per_solve": n / n_prof, "avg_launch_ms": ms / n,
+                 "share_of_kernel_time": ms / total_ms if total_ms > 0 else None}
+            if k in pb:
+                bpl = pb[k] * n_prof / n
+                ach = bpl / (ms / n / 1e3) / 1e9
+                e.update({"bytes_per_launch": bpl, "achieved_gbs": ach, "frac": ach / HBM_PEAK_GBS})
+            kernels[k] = e
+        dom = max((k for k in kernels if "achieved_gbs" in kernels[k]), key=lambda k: kernels[k]["ms_per_solve"])
+        dominant = dict(name=dom, **kernels[dom])
+        dominant["single_stream_ms_per_solve"] = t_single * 1e3
+        psolver.close()
+        if args.profile_only:
+            if rank == 0:
+                print(json.dumps({"profile_only": True, "kernels": kernels, "dominant": dominant}), flush=True)
+            if world > 1:
+                dist.destroy_process_group()
+            return
+
+    value = B * args.steps / elapsed
+    traffic = pmc_traffic(args.variant, args.contact, B, N) if world == 1 else None
+    roofline = {
+        "bound": "hbm",
+        "scope": "whole solve: algorithmic bytes of every kernel (SURVEY.md §8(d) per-node words x device-counted "
+                 "calcDiffs / backward passes / line-search launches and step lengths, all ranks) / wall time "
+                 "of the timed region",
+        "achieved": tot_bytes * args.steps / elapsed / 1e9,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": tot_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
+        "traffic": (sum(v for v in traffic.values() if v) if traffic else None),
+        "bytes_per_step": tot_bytes,
+        "frac_survey_formula": tot_survey * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
+        "frac_of_measured_copy": tot_bytes * args.steps / elapsed / 1e9 / HBM_MEASURED_GBS,
+        "dominant_kernel": dominant,
+    }
+    if dominant is not None and traffic and traffic.get(dominant["name"]) is not None:
+        dominant["traffic_per_launch"] = traffic[dominant["name"]] / dominant["launches_per_solve"]
+
+    extras = {}
+    if not args.no_extras:
+        # SURVEY-literal random x0 regime, same global batch split
+        rb = make(B, SEED + 1, "random").slice(slice(b0, b1))
+        TR = tensors(rb)
+        rsolver = solver
+        rsolver.solve_dev(TR, maxiter=args.maxiter, stream=stream)
+        sync()
+        rs = 3
+        el = shard.timed_steps(lambda: rsolver.solve_dev(TR, maxiter=args.maxiter, stream=stream), rs, sync)
+        rok = float(shard.sum_over_ranks(torch.tensor([float(TR["ok"].sum().item())], **f64)).cpu()[0])
+        rit = float(shard.sum_over_ranks(torch.tensor([float(TR["iters"].sum().item())], **f64)).cpu()[0])
+        extras["random_regime"] = {"value": B * rs / el, "unit": "solves/s", "ms_per_step": el / rs * 1e3,
+                                   "ok_frac": rok / B, "mean_iter": rit / B}
+        del TR
+        if world > 1:
+            # weak scaling: every rank its own 4096-instance batch (distinct seeds)
+            wb = make(B, SEED + 100 + rank, args.regime)
+            TW = tensors(wb)
+            wsolver = BatchedBoxFDDP(cfg, max_batch=B, device=local_rank)
+            wsolver.solve_dev(TW, maxiter=args.maxiter, stream=stream)
+            sync()
+            ws = 3
+            el = shard.timed_steps(lambda: wsolver.solve_dev(TW, maxiter=args.maxiter, stream=stream), ws, sync)
+            extras["weak"] = {"value": B * world * ws / el, "unit": "solves/s", "batch_per_gpu": B,
+                              "ms_per_step": el / ws * 1e3}
+            wsolver.close()
+            del TW
 
     host_io = None
-    if not args.no_host_io:
+    if not args.no_host_io and world == 1:
         # PCIe-inclusive rate of the host-array entry point (ffddp_solve_batch):
         # H2D of the inputs + solve + D2H of xs/us/K/cost/...; reported beside
         # `value`, never as `value`.
-        solver.profile(False)
-        solver.solve(batch, maxiter=args.maxiter)
+        solver.solve(mine, maxiter=args.maxiter)
         th0 = time.perf_counter()
         reps = 3
         for _ in range(reps):
-            solver.solve(batch, maxiter=args.maxiter)
+            solver.solve(mine, maxiter=args.maxiter)
         th = (time.perf_counter() - th0) / reps
-        host_io = {"value": B / th, "unit": "solves/s", "ms_per_step": th * 1e3, "per_gpu": True}
+        host_io = {"value": mine.B / th, "unit": "solves/s", "ms_per_step": th * 1e3}
 
     if rank == 0:
         base = None
         if not args.no_cpu_baseline and world == 1:
-            base = cpu_baseline(args, shard.shard_seed(1234, rank))
+            base = cpu_baseline(cfg, glob, args.maxiter, args.cpu_budget)
         line = {
             "metric": METRIC,
             "value": value,
@@ -309,34 +359,37 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded workload.make_batch, tracking regime: x0 near IK of the benchmark "
-            "trajectory at t0~U(0,20)s; cold warm start)",
+            "data": f"synthetic (seeded workload.make_batch, {args.regime} regime"
+                    + (": x0 near IK of the benchmark trajectory at t0~U(0,20)s" if args.regime == "tracking" else "")
+                    + "; cold warm start)",
             "config": {
-                "workload": f"{args.variant} BoxFDDP solve, nx={nx} nu={nu}, horizon={N}, batch={B}/GPU, "
-                f"maxiter={args.maxiter}, contact={args.contact}",
+                "workload": f"{args.variant} BoxFDDP solve, nx={nx} nu={nu}, horizon={N}, global batch={B} split "
+                            f"over {world} GPU(s), maxiter={args.maxiter}, contact={args.contact}",
                 "variant": args.variant,
                 "horizon": N,
-                "batch_per_gpu": B,
-                "global_batch": B * world,
+                "global_batch": B,
+                "batch_per_gpu": counts,
                 "maxiter": args.maxiter,
                 "contact_model": args.contact,
-                "parallelism": f"shard{world}",
+                "parallelism": f"batch-split{world}",
+                "gather": args.gather if world > 1 else "none",
             },
             "roofline": roofline,
             "cpu_baseline": base,
             "solver": {
-                "ok_frac": float(np.mean(ok)),
-                "mean_iter": float(np.mean(iters)),
-                "mean_iters_run": float(np.mean(stats[:, 0])),
-                "mean_trials": float(np.mean(stats[:, 1])),
-                "mean_trials_evaluated": float(np.mean(stats[:, 6] + stats[:, 7])),
-                "cost_finite_frac": float(np.mean(np.isfinite(cost))),
+                "ok_frac": tot_ok / B,
+                "mean_iter": tot_it / B,
+                "rank0_mean_iters_run": float(np.mean(stats[:, 0])),
+                "rank0_mean_trials": float(np.mean(stats[:, 1])),
+                "rank0_mean_trials_evaluated": float(np.mean(stats[:, 6] + stats[:, 7])),
+                "rank0_cost_finite_frac": float(np.mean(np.isfinite(cost))),
             },
             "kernels": kernels,
             "host_io": host_io,
+            **extras,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,18 +1,26 @@
-"""Multi-GPU sharding of the batched solve.
+"""Multi-GPU partition of the batched solve.
 
-The OCP instances of a batch are independent, so N GPUs run N disjoint shards
-(one process per GPU, instance ids rank*B .. rank*B+B-1) with no collective in
-the data path.  The one exchange is the final all-gather of each instance's
-(cost, u0) — what a fleet-level MPC server returns to its callers — over RCCL
-(backend "nccl") on the GPU box, over gloo in the CPU tests.  Timing follows
-the bench contract: barrier + device sync on both sides of the timed region,
-elapsed = max over ranks.
+The OCP instances of a batch are independent, so G GPUs split one global
+batch of B instances into contiguous slices (one process per GPU, the
+remainder going to the last ranks) and solve them with no collective in the
+data path: strong scaling at fixed B, as BASELINE.json's metric ("batch=4096
+at 1/2/4/8 MI355X") asks.  The one exchange is the final all-gather of the
+per-instance results over RCCL (backend "nccl") on the GPU box, gloo in the
+CPU tests:
+  * "costs" (default): cost, iterations, ok and the first control u0 of every
+    instance — what a fleet-level MPC server returns to its callers;
+  * "full": the whole solution, xs, us, K and cost (117 MB at B = 4096,
+    N = 30), i.e. the reference solver's read-backs for every instance.
+Slices are padded to the largest slice for all_gather_into_tensor and
+unpadded in rank order.  Timing follows the bench contract: barrier + device
+sync on both sides of the timed region, elapsed = max over ranks.
+Replaces the single-process solve call at src/mpc/crocoddyl_classical.py:367.
 """
 from __future__ import annotations
 
 import os
 import time
-from typing import Callable, Optional
+from typing import Callable, Dict, Sequence
 
 import torch
 import torch.distributed as dist
@@ -35,28 +43,68 @@ def init(backend: str, local_rank: int, world: int):
         dist.init_process_group(backend)
 
 
-def shard_seed(base: int, rank: int) -> int:
-    return base + rank
+def slice_bounds(B: int, world: int, rank: int):
+    """Contiguous slice [b0, b1) of a global batch of B instances for `rank`
+    of `world`: floor(B / world) each, the remainder to the last ranks."""
+    base, rem = divmod(int(B), int(world))
+    extra_from = world - rem  # ranks >= extra_from get one more instance
+    b0 = rank * base + max(0, rank - extra_from)
+    return b0, b0 + base + (1 if rank >= extra_from else 0)
 
 
-def shard_range(rank: int, per_rank: int):
-    return rank * per_rank, (rank + 1) * per_rank
+def slice_counts(B: int, world: int):
+    return [slice_bounds(B, world, r)[1] - slice_bounds(B, world, r)[0] for r in range(world)]
 
 
-def gather_results(cost: torch.Tensor, u0: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """All-gather [cost | u0] of every shard -> (world, B, 1 + nu), rank order."""
-    local = torch.cat([cost[:, None], u0], 1).contiguous()
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    if world == 1:
-        return local[None]
-    if out is None:
-        out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
-    if dist.get_backend() == "nccl":
-        dist.all_gather_into_tensor(out, local)
+def pack_results(res: Dict[str, torch.Tensor], mode: str) -> torch.Tensor:
+    """Per-instance results -> one (B_local, W) float64 block.
+    costs: [cost, iters, ok, u0(7)];  full: [cost, xs, us, K]."""
+    B = res["cost"].shape[0]
+    cost = res["cost"].reshape(B, 1).to(torch.float64)
+    if mode == "costs":
+        parts = [cost, res["iters"].reshape(B, 1).to(torch.float64), res["ok"].reshape(B, 1).to(torch.float64),
+                 res["us"][:, 0, :].to(torch.float64)]
+    elif mode == "full":
+        parts = [cost] + [res[k].reshape(B, -1) for k in ("xs", "us", "K")]
     else:
-        parts = list(out.unbind(0))
-        dist.all_gather(parts, local)
-    return out
+        raise ValueError(mode)
+    return torch.cat(parts, 1).contiguous()
+
+
+def unpack_full(block: torch.Tensor, N: int, nx: int, nu: int = 7):
+    """Inverse of pack_results(..., "full") on a gathered (B, W) block."""
+    B = block.shape[0]
+    o = 1
+    xs = block[:, o:o + (N + 1) * nx].reshape(B, N + 1, nx)
+    o += (N + 1) * nx
+    us = block[:, o:o + N * nu].reshape(B, N, nu)
+    o += N * nu
+    K = block[:, o:o + N * nu * nx].reshape(B, N, nu, nx)
+    return dict(cost=block[:, 0], xs=xs, us=us, K=K)
+
+
+class Gatherer:
+    """All-gather of the packed per-instance results of every rank's slice
+    into the global batch order; buffers allocated once (bench reuses it
+    every step)."""
+
+    def __init__(self, counts: Sequence[int], width: int, device, dtype=torch.float64):
+        self.counts = list(counts)
+        self.world = len(self.counts)
+        self.maxB = max(self.counts)
+        self.send = torch.zeros((self.maxB, width), dtype=dtype, device=device)
+        self.recv = torch.zeros((self.world, self.maxB, width), dtype=dtype, device=device)
+
+    def __call__(self, local: torch.Tensor) -> torch.Tensor:
+        n = local.shape[0]
+        if self.world == 1:
+            return local
+        self.send[:n].copy_(local)
+        if dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(self.recv, self.send)
+        else:
+            dist.all_gather(list(self.recv.unbind(0)), self.send)
+        return torch.cat([self.recv[r, :c] for r, c in enumerate(self.counts)], 0)
 
 
 def timed_steps(step: Callable[[], None], steps: int, sync: Callable[[], None]) -> float:
@@ -78,3 +126,11 @@ def timed_steps(step: Callable[[], None], steps: int, sync: Callable[[], None]) 
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
+
+
+def sum_over_ranks(x: torch.Tensor) -> torch.Tensor:
+    """Element-wise sum over ranks (identity on one process)."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        x = x.clone()
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+    return x

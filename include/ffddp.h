@@ -140,7 +140,8 @@ const char* ffddp_last_error(const ffddp_handle* h);
  *                    [1] line-search trials a sequential solver executes,
  *                    [2] regularisation retries of the backward pass,
  *                    [3] backward passes run, [4] calcDiff evaluations,
- *                    [5] forward (line-search) launches,
+ *                    [5] line-search kernel launches that processed the
+ *                    instance (first pass + second pass when it ran),
  *                    [6] / [7] step lengths evaluated by the first / second
  *                    line-search pass — for the roofline byte count
  *                    (SURVEY.md §8(d)). */

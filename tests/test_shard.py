@@ -1,10 +1,12 @@
-"""world_size-2 gloo run of the sharded solve path (ffddp.shard) on CPU.
+"""world_size-2 gloo run of the partitioned solve path (ffddp.shard) on CPU.
 
-Each rank builds its own seeded shard, solves it (the numpy oracle stands in
-for the HIP kernel here — there is no GPU in this test), all-gathers
-(cost, u0) and times its steps with the bench fences.  Rank 0 checks that the
-gathered block of every rank equals an independent recomputation of that
-rank's shard, and that the timed elapsed is the max over ranks."""
+One global batch of B instances is split into contiguous slices (remainder to
+the last ranks); each rank solves its slice (the numpy oracle stands in for
+the HIP kernel here — there is no GPU in this test), all-gathers the packed
+results in both modes ("costs": cost, iters, ok, u0; "full": cost, xs, us,
+K) and times its steps with the bench fences.  Rank 0 checks the gathered
+global arrays against an independent single-process solve of the whole
+batch, and that the timed elapsed is the max over ranks."""
 from __future__ import annotations
 
 import os
@@ -13,12 +15,12 @@ import sys
 from pathlib import Path
 
 import numpy as np
-import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 ROOT = Path(__file__).resolve().parents[1]
+B_GLOBAL, N = 5, 4
 
 
 def _free_port():
@@ -29,20 +31,21 @@ def _free_port():
     return p
 
 
-def _solve_shard(rank, B, N):
+def _solve(idx):
+    """Oracle solves of global instances idx -> result tensors (the solver outputs bench gathers)."""
     from helpers import make_batch, oracle_solve, product_cfg
-    from ffddp import shard, workload  # noqa: F401
 
     cfg = product_cfg("classical", N)
-    b = make_batch("classical", B, N, seed=shard.shard_seed(1234, rank))
-    cost, u0 = np.zeros(B), np.zeros((B, 7))
-    for i in range(B):
-        _, s = oracle_solve(cfg, b, i, maxiter=2)
-        cost[i], u0[i] = s.cost, s.us[0]
-    return cost, u0
+    b = make_batch("classical", B_GLOBAL, N, seed=1234)
+    res = dict(cost=[], iters=[], ok=[], xs=[], us=[], K=[])
+    for i in idx:
+        ok, s = oracle_solve(cfg, b, int(i), maxiter=2)
+        for k, v in (("cost", s.cost), ("iters", s.iter), ("ok", ok), ("xs", s.xs), ("us", s.us), ("K", s.K)):
+            res[k].append(v)
+    return {k: torch.tensor(np.array(v, dtype=np.float64)) for k, v in res.items()}
 
 
-def _worker(rank, world, port, B, N, q):
+def _worker(rank, world, port, q):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "tests"))
     import ffddp_path  # noqa: F401
@@ -53,49 +56,75 @@ def _worker(rank, world, port, B, N, q):
     r, w, lr = shard.env_ranks()
     shard.init("gloo", lr, w)
     try:
-        cost, u0 = _solve_shard(r, B, N)
-        out = shard.gather_results(torch.tensor(cost), torch.tensor(u0))
+        b0, b1 = shard.slice_bounds(B_GLOBAL, w, r)
+        res = _solve(range(b0, b1))
+        counts = shard.slice_counts(B_GLOBAL, w)
+        out = {}
+        for mode in ("costs", "full"):
+            local = shard.pack_results(res, mode)
+            out[mode] = shard.Gatherer(counts, local.shape[1], "cpu")(local).numpy()
         slow = 0.3 if r == 1 else 0.0
         import time
 
         elapsed = shard.timed_steps(lambda: time.sleep(slow), 1, lambda: None)
-        q.put((r, out.numpy(), elapsed))
+        tot = shard.sum_over_ranks(torch.tensor([float(b1 - b0)])).item()
+        q.put((r, (b0, b1), out, elapsed, tot))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_gather_and_timing():
-    world, B, N = 2, 2, 4
+def test_two_rank_strong_split_and_gathers():
+    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, N, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(world):
-        r, out, el = q.get(timeout=300)
-        res[r] = (out, el)
+        r, bounds, out, el, tot = q.get(timeout=300)
+        res[r] = (bounds, out, el, tot)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    out0, el0 = res[0]
-    out1, el1 = res[1]
-    assert out0.shape == (world, B, 8)
-    np.testing.assert_array_equal(out0, out1)
+    # contiguous slices covering the global batch, remainder on the last rank
+    assert res[0][0] == (0, 2) and res[1][0] == (2, 5)
+    assert res[0][3] == res[1][3] == B_GLOBAL
+    from ffddp import shard
+
+    ref = _solve(range(B_GLOBAL))
     for r in range(world):
-        cost, u0 = _solve_shard(r, B, N)
-        np.testing.assert_array_equal(out0[r, :, 0], cost)
-        np.testing.assert_array_equal(out0[r, :, 1:], u0)
-    # shards differ (distinct seeds) and the timing is the max over ranks
-    assert not np.array_equal(out0[0], out0[1])
-    assert el0 == el1 and el0 >= 0.3
+        out = res[r][1]
+        assert out["costs"].shape == (B_GLOBAL, 10)
+        assert out["full"].shape == (B_GLOBAL, 1 + (N + 1) * 14 + N * 7 + N * 7 * 14)
+        np.testing.assert_array_equal(out["costs"][:, 0], ref["cost"].numpy())
+        np.testing.assert_array_equal(out["costs"][:, 1], ref["iters"].numpy())
+        np.testing.assert_array_equal(out["costs"][:, 3:], ref["us"].numpy()[:, 0])
+        full = shard.unpack_full(torch.tensor(out["full"]), N, 14)
+        for k in ("cost", "xs", "us", "K"):
+            np.testing.assert_array_equal(full[k].numpy(), ref[k].numpy())
+    # the timing is the max over ranks
+    assert res[0][2] == res[1][2] and res[0][2] >= 0.3
+
+
+def test_slice_bounds_partition():
+    from ffddp import shard
+
+    for B in (1, 7, 512, 4096, 4097):
+        for world in (1, 2, 3, 4, 8):
+            b = [shard.slice_bounds(B, world, r) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == B
+            assert all(b[r][1] == b[r + 1][0] for r in range(world - 1))
+            c = shard.slice_counts(B, world)
+            assert max(c) - min(c) <= 1 and c == sorted(c)  # remainder on the last ranks
+    assert shard.slice_bounds(4096, 8, 3) == (1536, 2048)
 
 
 def test_single_rank_passthrough():
-    import ffddp_path  # noqa: F401
     from ffddp import shard
 
-    out = shard.gather_results(torch.arange(3.0), torch.ones(3, 7))
-    assert out.shape == (1, 3, 8)
-    assert shard.shard_range(2, 4096) == (8192, 12288)
+    res = dict(cost=torch.arange(3.0), iters=torch.ones(3), ok=torch.ones(3), us=torch.ones(3, 4, 7))
+    local = shard.pack_results(res, "costs")
+    assert local.shape == (3, 10)
+    assert torch.equal(shard.Gatherer([3], 10, "cpu")(local), local)
