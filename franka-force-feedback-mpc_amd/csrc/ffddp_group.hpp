@@ -29,19 +29,43 @@ __device__ __forceinline__ int g8_lane() { return (int)(threadIdx.x & 7); }
 // DPP rows; lanes whose source falls outside the group are masked by the
 // callers), ds_swizzle BROADCAST(8, k) for broadcasts, DPP half-mirror and
 // quad permutes for the sums.
+// bound_ctrl: a lane whose source is outside the row reads 0 (what the scans
+// need), and no "old" operand has to be zeroed first: one v_mov_b32_dpp per
+// 32-bit half and nothing else (with update_dpp(0, ...) every move also cost
+// two v_mov_b32 of the zero old value; a VALU op is 4 cycles of the wave
+// either way, so those were a third of every scan step)
 template <int CTRL> __device__ __forceinline__ double dpp64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 template <int CTRL> __device__ __forceinline__ int dpp32(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true);
 }
+#ifndef G8_DPP
+#define G8_DPP 0
+#endif
+// Broadcast of group lane K.  ds_swizzle BROADCAST(8, K) by default; with
+// G8_DPP two DPP moves instead (quad_perm [k,k,k,k] gives every quad its lane
+// K & 3, then the quad of the group that does not hold lane K takes the
+// other quad's value by row_shr:4 / row_shl:4 under a bank mask; groups are
+// 8-aligned inside 16-lane DPP rows).  Measured: no faster.
 template <int K> __device__ __forceinline__ double g8_bc(double v) {
+#if G8_DPP
+  constexpr int qp = (K & 3) * 0x55;
+  constexpr int sh = K < 4 ? 0x114 : 0x104;
+  constexpr int bm = K < 4 ? 0xA : 0x5;
+  int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), qp, 0xf, 0xf, false);
+  int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), qp, 0xf, 0xf, false);
+  lo = __builtin_amdgcn_update_dpp(lo, lo, sh, 0xf, bm, false);
+  hi = __builtin_amdgcn_update_dpp(hi, hi, sh, 0xf, bm, false);
+  return __hiloint2double(hi, lo);
+#else
   constexpr int off = 0x18 | (K << 5);  // swizzle bitmask mode: and 0x18, or K
   const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), off);
   const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), off);
   return __hiloint2double(hi, lo);
+#endif
 }
 __device__ __forceinline__ double g8_get(double v, int src) {
   switch (src) {

@@ -380,10 +380,23 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
 __device__ __forceinline__ bool bad(double v) { return isnan(v) || isinf(v) || v >= 1e30; }
 
 
+// sum over the 64 lanes, wave-uniform result: DPP butterflies inside each
+// 16-lane row (quad swaps, half-row and row mirrors), then the four row sums
+// by readlane -- no ds_bpermute round trips on the backward pass's chain
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp64<0x141>(v);  // row_half_mirror
+  v += dpp64<0x140>(v);  // row_mirror
+  const double r0 = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 0),
+                                     __builtin_amdgcn_readlane(__double2loint(v), 0));
+  const double r1 = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 16),
+                                     __builtin_amdgcn_readlane(__double2loint(v), 16));
+  const double r2 = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 32),
+                                     __builtin_amdgcn_readlane(__double2loint(v), 32));
+  const double r3 = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 48),
+                                     __builtin_amdgcn_readlane(__double2loint(v), 48));
+  return (r0 + r1) + (r2 + r3);
 }
 
 // ---------------------------------------------------------------------------
