@@ -75,9 +75,11 @@ FFD_HD void log3(const double* R, double* r, double& th) {
   const double tr = R[0] + R[4] + R[8];
   double c = (tr - 1.0) / 2.0;
   c = c > 1.0 ? 1.0 : (c < -1.0 ? -1.0 : c);
-  th = acos(c);
+  th = acos_(c);
   const double eps3 = 6.0554544523933395e-06;  // eps^(1/3)
-  const double t = (th > eps3 ? th / sin(th) : 1.0) / 2.0;
+  double st, ct;
+  sincos_(th, st, ct);
+  const double t = (th > eps3 ? th / st : 1.0) / 2.0;
   r[0] = t * (R[7] - R[5]);
   r[1] = t * (R[2] - R[6]);
   r[2] = t * (R[3] - R[1]);
@@ -87,7 +89,8 @@ FFD_HD void jlog3(const double* r, double th, double* J) {
   const double eps3 = 6.0554544523933395e-06;
   double alpha, beta;
   if (th >= eps3) {
-    const double st = sin(th), ct = cos(th);
+    double st, ct;
+    sincos_(th, st, ct);
     const double st_1mct = st / (1.0 - ct);
     alpha = th * st_1mct / 2.0;
     beta = 1.0 / (th * th) - st_1mct / (2.0 * th);
