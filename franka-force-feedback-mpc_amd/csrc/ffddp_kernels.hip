@@ -84,7 +84,25 @@ struct Dev {
   InstState* st;     // [B]
   Primal* prim;      // [B][N+1]  node calc (primal) results for the calcDiff tangents
   double* link;      // [B][N+1][LK_ALLOC]  per-link world-frame data (rb_links) for the tangents
+  int* alist;        // [2][B]  active-instance lists (slice-local indices), double-buffered over iterations
+  int* acnt;         // [2]     their lengths
 };
+
+// Active-instance compaction.  Iteration it reads list (it & 1): the
+// instances not yet done, packed at the front, so the blocks / groups of the
+// per-iteration kernels that carry work are the first ones of the grid and
+// the rest exit at once.  Without it a late iteration's few active
+// instances are scattered over the whole grid, and a grid larger than one
+// wave per SIMD (the 1-wave/SIMD line search with 4 trials) ran its active
+// waves in two dispatch rounds.  k_accept_commit appends the instances that
+// continue to the other list; k_backward_w zeroes that list's length first.
+struct ActiveList {
+  const int* list;
+  int n;
+};
+__device__ __forceinline__ ActiveList active_list(const Dev& d, int cur) {
+  return ActiveList{d.alist + (long)cur * d.B, d.acnt[cur]};
+}
 
 // ---------------------------------------------------------------------------
 // init
@@ -104,6 +122,11 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
     }
     d.K[i] = 0.0;
     if (i < d.B) {
+      d.alist[i] = (int)i;
+      if (i == 0) {
+        d.acnt[0] = d.B;
+        d.acnt[1] = 0;
+      }
       InstState s;
       s.preg = C.reg_min;
       s.cost = 0.0;
@@ -150,16 +173,23 @@ struct NodeShared {
 template <int NC, bool FF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_G8_WAVES))) void k_primal_g8(
     const DevConsts* __restrict__ Cg, Dev d, const double* __restrict__ x0, const double* __restrict__ node_ref,
-    const double* __restrict__ inst_ref, const uint8_t* __restrict__ surface, int force_all) {
+    const double* __restrict__ inst_ref, const uint8_t* __restrict__ surface, int force_all, int cur) {
   const DevConsts& C = *Cg;
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
-  const long node = (blockIdx.x * (long)blockDim.x + threadIdx.x) / G8;
+  const long gnode = (blockIdx.x * (long)blockDim.x + threadIdx.x) / G8;
   const int li = g8_lane();
   const bool J = li < NQ;
   const int ji = J ? li : 0;
-  const int b = (int)(node / (N + 1)), t = (int)(node % (N + 1));
-  if (b >= d.B) return;
+  const int slot = (int)(gnode / (N + 1)), t = (int)(gnode % (N + 1));
+  if (slot >= d.B) return;
+  int b = slot;
+  if (!force_all) {
+    const ActiveList al = active_list(d, cur);
+    if (slot >= al.n) return;
+    b = al.list[slot];
+  }
+  const long node = (long)b * (N + 1) + t;
   if (!force_all && (d.st[b].done != 0 || d.st[b].recalc == 0)) return;
   const bool surf = surface[b] != 0;
   const bool terminal = t == N;
@@ -246,17 +276,24 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
                                                       const double* __restrict__ x0,
                                                       const double* __restrict__ node_ref,
                                                       const double* __restrict__ inst_ref,
-                                                      const uint8_t* __restrict__ surface, int force_all) {
+                                                      const uint8_t* __restrict__ surface, int force_all, int cur) {
   const DevConsts& C = *Cg;
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
   constexpr int nc = NC;
   __shared__ NodeShared S;
   const int grp = threadIdx.x / NODE_GROUP, lane = threadIdx.x % NODE_GROUP;
-  const long node = (long)blockIdx.x * NODE_GPB + grp;
-  const int b = (int)(node / (N + 1)), t = (int)(node % (N + 1));
-  bool active = b < d.B;
-  if (active && !force_all) active = (d.st[b].done == 0) && (d.st[b].recalc != 0);
+  const long gnode = (long)blockIdx.x * NODE_GPB + grp;
+  const int slot = (int)(gnode / (N + 1)), t = (int)(gnode % (N + 1));
+  int b = slot;
+  bool active = slot < d.B;
+  if (active && !force_all) {
+    const ActiveList al = active_list(d, cur);
+    active = slot < al.n;
+    b = active ? al.list[slot] : 0;
+    if (active) active = (d.st[b].done == 0) && (d.st[b].recalc != 0);
+  }
+  const long node = (long)b * (N + 1) + t;
   const bool surf = active ? surface[b] != 0 : false;
   const bool terminal = t == N;
   constexpr bool ff = FF;
@@ -633,14 +670,17 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
 }
 
 template <bool FF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_WAVES))) void k_backward_w(const DevConsts* __restrict__ Cg, Dev d, int iter) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_WAVES))) void k_backward_w(const DevConsts* __restrict__ Cg, Dev d, int iter, int cur) {
   using S_t = BwW<FF>;
   constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
   constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane
   const DevConsts& C = *Cg;
   const int N = C.N;
-  const int b = blockIdx.x, l = threadIdx.x;
-  if (b >= d.B) return;
+  const int l = threadIdx.x;
+  if (blockIdx.x == 0 && l == 0) d.acnt[cur ^ 1] = 0;  // the list k_accept_commit builds
+  const ActiveList al = active_list(d, cur);
+  if ((int)blockIdx.x >= al.n) return;
+  const int b = al.list[blockIdx.x];
   InstState* st = d.st + b;
   if (st->done) return;
 #ifdef FFDDP_PHASE_PROF
@@ -1014,7 +1054,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_
                                                    const double* __restrict__ node_ref,
                                                    const double* __restrict__ inst_ref,
                                                    const uint8_t* __restrict__ surface, int tr0, int ntr,
-                                                   int only_more) {
+                                                   int only_more, int cur) {
   const DevConsts& C = *Cg;
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
@@ -1022,8 +1062,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_
   const int li = g8_lane();
   const bool J = li < NQ;
   const int ji = J ? li : 0;
-  const int b = (int)(gid / ntr), tr = tr0 + (int)(gid % ntr);
-  if (b >= d.B) return;
+  const int slot = (int)(gid / ntr), tr = tr0 + (int)(gid % ntr);
+  const ActiveList al = active_list(d, cur);
+  if (slot >= al.n) return;
+  const int b = al.list[slot];
   const InstState* st = d.st + b;
   if (st->done) return;
   if (only_more) {
@@ -1234,12 +1276,16 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int 
 
 // acceptance (lane 0) + setCandidate copy of the accepted trial into (xs, us)
 // by the whole block: one block per instance
-__global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1) {
+__global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1, int cur) {
   const DevConsts& C = *Cg;
-  const int b = blockIdx.x;
-  if (b >= d.B) return;
+  const ActiveList al = active_list(d, cur);
+  if ((int)blockIdx.x >= al.n) return;
+  const int b = al.list[blockIdx.x];
   __shared__ int acc_s;
-  if (threadIdx.x == 0) acc_s = accept_instance(C, d, b, iter, n1);
+  if (threadIdx.x == 0) {
+    acc_s = accept_instance(C, d, b, iter, n1);
+    if (!d.st[b].done) d.alist[(long)(cur ^ 1) * d.B + atomicAdd(d.acnt + (cur ^ 1), 1)] = b;
+  }
   __syncthreads();
   const int acc = acc_s;
   if (acc < 0) return;
@@ -1491,7 +1537,7 @@ template <class T> int dalloc(ffddp_handle* h, T** p, size_t n) {
 }
 
 void free_all(ffddp_handle* h) {
-  void* ps[] = {h->dc, h->drb, h->d.prim, h->d.link, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
+  void* ps[] = {h->dc, h->drb, h->d.prim, h->d.link, h->d.alist, h->d.acnt, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
                 h->d.us_try, h->d.trial, h->d.trial_fail, h->d.st, h->in_x0, h->in_nref, h->in_iref, h->in_xs,
                 h->in_us, h->in_surf, h->out_xs, h->out_us, h->out_K, h->out_cost, h->out_fn, h->out_iters,
                 h->out_stats, h->out_ok};
@@ -1528,7 +1574,7 @@ struct ProfScope {
 enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE, KC_FORWARD2, KC_PRIMAL };
 
 // the per-instance slice [b0, b0 + Bk) of the handle workspace
-Dev dev_slice(const Dev& d0, int b0, int Bk) {
+Dev dev_slice(const Dev& d0, int b0, int Bk, int k) {
   Dev d = d0;
   const long N = d0.N, nx = d0.nx;
   d.B = Bk;
@@ -1546,6 +1592,8 @@ Dev dev_slice(const Dev& d0, int b0, int Bk) {
   d.st += b0;
   d.prim += (long)b0 * (N + 1);
   d.link += (long)b0 * (N + 1) * LK_ALLOC;
+  d.alist += 2L * b0;
+  d.acnt += 2 * k;
   return d;
 }
 
@@ -1584,7 +1632,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
   for (int k = 0; k < S; ++k) {
     sl[k].b0 = k * Bs;
     sl[k].B = (B - sl[k].b0) < Bs ? (B - sl[k].b0) : Bs;
-    sl[k].d = dev_slice(h->d, sl[k].b0, sl[k].B);
+    sl[k].d = dev_slice(h->d, sl[k].b0, sl[k].B, k);
     // FFDDP_CALLER_SLICE: the last slice runs on the caller's stream (its
     // hardware queue is otherwise idle during the solve)
     sl[k].s = (S > 1 && !(h->caller_slice && k == S - 1)) ? h->streams[k] : s;
@@ -1618,18 +1666,18 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       {
         ProfScope p(h, ss, KC_PRIMAL);
         hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k,
-                           nrefk, irefk, surfk, 0);
+                           nrefk, irefk, surfk, 0, it & 1);
       }
       if (it == 0 && h->stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_NODE);
         hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, ss,
-                           h->dc, d, x0k, nrefk, irefk, surfk, 0);
+                           h->dc, d, x0k, nrefk, irefk, surfk, 0, it & 1);
       }
       if (it == 0 && h->stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_BACKWARD);
-        hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it);
+        hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1);
       }
       int n1 = NTRIALS;
       {
@@ -1642,10 +1690,10 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
           const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
           if (late)
             hipLaunchKernelGGL((k_forward_g8<NC, FF, 1, true>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
-                               surfk, tr0, ntr, more);
+                               surfk, tr0, ntr, more, it & 1);
           else
             hipLaunchKernelGGL((k_forward_g8<NC, FF>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk, tr0,
-                               ntr, more);
+                               ntr, more, it & 1);
         };
         {
           ProfScope p(h, ss, KC_FORWARD);
@@ -1658,7 +1706,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       }
       {
         ProfScope p(h, ss, KC_ACCEPT);
-        hipLaunchKernelGGL(k_accept_commit, dim3(Bk), dim3(64), 0, ss, h->dc, d, it, n1);
+        hipLaunchKernelGGL(k_accept_commit, dim3(Bk), dim3(64), 0, ss, h->dc, d, it, n1, it & 1);
       }
     }
   }
@@ -1708,9 +1756,9 @@ template <int NC, bool FF>
 void launch_node(ffddp_handle* h, Dev d, int B, hipStream_t s, int force_all) {
   const long nodes = (long)B * (h->hc.N + 1);
   hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
-                     h->in_nref, h->in_iref, h->in_surf, force_all);
+                     h->in_nref, h->in_iref, h->in_surf, force_all, 0);
   hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, s, h->dc,
-                     d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all);
+                     d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all, 0);
 }
 
 bool valid_cfg(const ffddp_ocp_config& c) {
@@ -1786,6 +1834,8 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   rc |= dalloc(h, &d.trial_fail, (size_t)B * NTRIALS);
   rc |= dalloc(h, &d.st, (size_t)B);
   rc |= dalloc(h, &d.prim, (size_t)B * (N + 1));
+  rc |= dalloc(h, &d.alist, (size_t)B * 2);
+  rc |= dalloc(h, &d.acnt, (size_t)2 * 8);
   rc |= dalloc(h, &h->in_x0, (size_t)B * nx);
   rc |= dalloc(h, &h->in_nref, (size_t)B * (N + 1) * 6);
   rc |= dalloc(h, &h->in_iref, (size_t)B * 21);
