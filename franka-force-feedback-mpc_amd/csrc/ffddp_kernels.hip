@@ -1274,20 +1274,41 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int 
   return acc;
 }
 
-// acceptance (lane 0) + setCandidate copy of the accepted trial into (xs, us)
-// by the whole block: one block per instance
-__global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1, int cur) {
+// acceptance + setCandidate copy of the accepted trial into (xs, us):
+// ACC_IPB instances per 64-lane block, a 16-lane quarter each (its lane 0
+// decides, the quarter copies); the block appends its continuing instances to
+// the next active list with ONE atomic (one atomic per instance made the
+// 4096-instance launch 3x slower; 256-thread blocks instead waited for free
+// CU slots behind the other slices' node kernels)
+constexpr int ACC_IPB = 4;
+__global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1,
+                                                      int cur) {
   const DevConsts& C = *Cg;
   const ActiveList al = active_list(d, cur);
-  if ((int)blockIdx.x >= al.n) return;
-  const int b = al.list[blockIdx.x];
-  __shared__ int acc_s;
-  if (threadIdx.x == 0) {
-    acc_s = accept_instance(C, d, b, iter, n1);
-    if (!d.st[b].done) d.alist[(long)(cur ^ 1) * d.B + atomicAdd(d.acnt + (cur ^ 1), 1)] = b;
+  const int q = threadIdx.x / 16, l = threadIdx.x % 16;
+  const int slot = (int)blockIdx.x * ACC_IPB + q;
+  if ((int)blockIdx.x * ACC_IPB >= al.n) return;
+  const bool has = slot < al.n;
+  const int b = has ? al.list[slot] : 0;
+  __shared__ int acc_s[ACC_IPB], cont_s[ACC_IPB];
+  if (l == 0) {
+    acc_s[q] = has ? accept_instance(C, d, b, iter, n1) : -1;
+    cont_s[q] = (has && !d.st[b].done) ? 1 : 0;
   }
   __syncthreads();
-  const int acc = acc_s;
+  if (threadIdx.x == 0) {
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < ACC_IPB; ++i) n += cont_s[i];
+    if (n > 0) {
+      int pos = atomicAdd(d.acnt + (cur ^ 1), n);
+      int* next = d.alist + (long)(cur ^ 1) * d.B;
+#pragma unroll
+      for (int i = 0; i < ACC_IPB; ++i)
+        if (cont_s[i]) next[pos++] = al.list[(int)blockIdx.x * ACC_IPB + i];
+    }
+  }
+  const int acc = acc_s[q];
   if (acc < 0) return;
   const int N = C.N, nx = C.nx;
   const long perX = (long)(N + 1) * nx, perU = (long)N * NU;
@@ -1295,8 +1316,8 @@ __global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restric
   const double* su = d.us_try + ((long)b * NTRIALS + acc) * perU;
   double* dx = d.xs + (long)b * perX;
   double* du = d.us + (long)b * perU;
-  for (long i = threadIdx.x; i < perX; i += blockDim.x) dx[i] = sx[i];
-  for (long i = threadIdx.x; i < perU; i += blockDim.x) du[i] = su[i];
+  for (long i = l; i < perX; i += 16) dx[i] = sx[i];
+  for (long i = l; i < perU; i += 16) du[i] = su[i];
 }
 
 // solution read-back helpers: iter/ok, contact force at knots 0 and 1
@@ -1706,7 +1727,8 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       }
       {
         ProfScope p(h, ss, KC_ACCEPT);
-        hipLaunchKernelGGL(k_accept_commit, dim3(Bk), dim3(64), 0, ss, h->dc, d, it, n1, it & 1);
+        hipLaunchKernelGGL(k_accept_commit, dim3((Bk + ACC_IPB - 1) / ACC_IPB), dim3(64), 0, ss, h->dc, d, it, n1,
+                           it & 1);
       }
     }
   }
