@@ -62,8 +62,7 @@ def algorithmic_words(nx: int, nu: int, N: int):
     io = nx + (N + 1) * nx + N * nu + (N + 1) * 6 + 21 + (N + 1) * nx + N * nu + N * nu * nx + 1
     C_shared = N * (3 * nx + 2 * nu + nu * nx + 6) + (3 * nx + 6)
     C_trial = N * (nx + nu) + nx
-    return dict(A=A, B=Bw, C=Cf, A_T=A_T, B_T=B_T, C_T=C_T, IO=io, C_shared=C_shared, C_trial=C_trial,
-                primal=2 * nx + nu + 6 + nx + 1)
+    return dict(A=A, B=Bw, C=Cf, A_T=A_T, B_T=B_T, C_T=C_T, IO=io, C_shared=C_shared, C_trial=C_trial)
 
 
 def solve_bytes(stats: np.ndarray, nx: int, nu: int, N: int) -> dict:
@@ -75,17 +74,15 @@ def solve_bytes(stats: np.ndarray, nx: int, nu: int, N: int) -> dict:
     w = algorithmic_words(nx, nu, N)
     s = stats.astype(np.float64)
     n_calc, n_bw, n_fw, ev1, ev2 = s[:, 4].sum(), s[:, 0].sum(), s[:, 5].sum(), s[:, 6].sum(), s[:, 7].sum()
-    calc = 8.0 * n_calc * (N * w["A"] + w["A_T"])
-    primal = 8.0 * n_calc * (N + 1) * w["primal"]
+    calc = 8.0 * n_calc * (N * w["A"] + w["A_T"])  # k_node: calc + calcDiff, fused
     out = {
-        "primal": primal,
-        "node": calc - primal,
+        "node": calc,
         "backward": 8.0 * n_bw * (N * w["B"] + w["B_T"]),
         "forward": 8.0 * (n_bw * w["C_shared"] + ev1 * w["C_trial"]),
         "forward2": 8.0 * ((n_fw - n_bw) * w["C_shared"] + ev2 * w["C_trial"]),
         "io": 8.0 * stats.shape[0] * w["IO"],
     }
-    out["total"] = out["primal"] + out["node"] + out["backward"] + out["forward"] + out["forward2"] + out["io"]
+    out["total"] = out["node"] + out["backward"] + out["forward"] + out["forward2"] + out["io"]
     # SURVEY §8(d) literal: every evaluated step length reads its inputs again
     out["total_survey_formula"] = 8.0 * (n_calc * (N * w["A"] + w["A_T"]) + n_bw * (N * w["B"] + w["B_T"]) +
                                          (ev1 + ev2) * (N * w["C"] + w["C_T"]) + stats.shape[0] * w["IO"])

@@ -6,11 +6,11 @@
 // iteration; all per-instance control flow (regularisation, line-search
 // acceptance, feasibility, stopping) lives on the device, masked per instance:
 //
-//   k_primal_g8 calc of every (instance, node) on an 8-lane group (joint
-//               lanes + EE lane, log-depth scans): dynamics, costs, gaps.
-//   k_node      calcDiff of every (instance, node): 16-lane group per node,
-//               lane j computes state direction j in closed form (Jacobian
-//               column j), Gauss-Newton Hessians assembled across the group in LDS.
+//   k_node      calc + calcDiff of every (instance, node), 16-lane group per
+//               node: lanes 0..7 run the calc (joint lanes + EE lane, log-depth
+//               scans: dynamics, costs, gaps) into the group's LDS, then lane j
+//               computes state direction j in closed form (Jacobian column j)
+//               and the Gauss-Newton Hessians are assembled across the group.
 //   k_backward_w  Riccati backward pass, one wavefront per instance, blocks in
 //               LDS; Cholesky (infeasible iterations) or BoxQP gains;
 //               regularisation retries inside the kernel.
@@ -50,9 +50,6 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 #ifndef FW_WAVES
 #define FW_WAVES 2
 #endif
-#ifndef PRIMAL_G8_WAVES
-#define PRIMAL_G8_WAVES 2
-#endif
 #ifndef QC_UNROLL
 #define QC_UNROLL 1
 #endif
@@ -82,8 +79,6 @@ struct Dev {
   double* trial;     // [B][T][2]  cost_try, dv
   int* trial_fail;   // [B][T]
   InstState* st;     // [B]
-  Primal* prim;      // [B][N+1]  node calc (primal) results for the calcDiff tangents
-  double* link;      // [B][N+1][LK_ALLOC]  per-link world-frame data (rb_links) for the tangents
   int* alist;        // [2][B]  active-instance lists (slice-local indices), double-buffered over iterations
   int* acnt;         // [2]     their lengths
 };
@@ -168,29 +163,19 @@ struct NodeShared {
   NodeGroupShared g[NODE_GPB];
 };
 
-// k_primal on 8-lane groups (ffddp_primal_g8.hpp): one group per node, the
-// rigid-body recursions as log-depth scans; same outputs as k_primal.
+// The calc of one node on an 8-lane group (lanes = joints + EE): dynamics,
+// costs with their Gauss-Newton weights, gaps; Primal and link record to P /
+// lk (the node group's LDS in k_node).
 template <int NC, bool FF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_G8_WAVES))) void k_primal_g8(
-    const DevConsts* __restrict__ Cg, Dev d, const double* __restrict__ x0, const double* __restrict__ node_ref,
-    const double* __restrict__ inst_ref, const uint8_t* __restrict__ surface, int force_all, int cur) {
-  const DevConsts& C = *Cg;
+__device__ __forceinline__ void primal_group(const DevConsts& C, const Dev& d, const double* __restrict__ x0,
+                                             const double* __restrict__ node_ref, const double* __restrict__ inst_ref,
+                                             const uint8_t* __restrict__ surface, int b, int t, Primal* P,
+                                             double* lk) {
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
-  const long gnode = (blockIdx.x * (long)blockDim.x + threadIdx.x) / G8;
   const int li = g8_lane();
   const bool J = li < NQ;
   const int ji = J ? li : 0;
-  const int slot = (int)(gnode / (N + 1)), t = (int)(gnode % (N + 1));
-  if (slot >= d.B) return;
-  int b = slot;
-  if (!force_all) {
-    const ActiveList al = active_list(d, cur);
-    if (slot >= al.n) return;
-    b = al.list[slot];
-  }
-  const long node = (long)b * (N + 1) + t;
-  if (!force_all && (d.st[b].done != 0 || d.st[b].recalc == 0)) return;
   const bool surf = surface[b] != 0;
   const bool terminal = t == N;
   const int mode = !terminal ? MODE_RUNNING : (FF ? MODE_TERMINAL_U : MODE_TERMINAL_X);
@@ -202,8 +187,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_G8_WA
   const double u = (uin != nullptr) ? uin[ji] : 0.0;
   double lam[3];
   const double pc = node_primal_g8<NC>(C, mode, surf, q, v, u, xreg[ji], xreg[7 + ji], xreg[14 + ji], ref,
-                                       d.prim + node, d.link + node * LK_ALLOC, lam);
-  double* rec = d.rec_buf + node * d.rec;
+                                       P, lk, lam);
+  double* rec = d.rec_buf + ((long)b * (N + 1) + t) * d.rec;
   // node cost (IAM scaling, FF augmentation terms): per-lane shares summed over the group
   double c = FF ? C.dt * pc : (terminal ? pc : C.dt * pc);
   if (FF) {
@@ -242,7 +227,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_G8_WA
       double* f = d.fs + ((long)b * (N + 1) + t + 1) * nx;
       const double* yn = d.xs + ((long)b * (N + 1) + t + 1) * nx;
       const double dt = C.dt;
-      const double a = d.prim[node].a[li];  // this lane's own store
+      const double a = P->a[li];  // this lane's own store
       const double qn = (mode == MODE_TERMINAL_X) ? q : q + (v * dt + a * dt * dt);
       const double vn = (mode == MODE_TERMINAL_X) ? v : v + a * dt;
       f[li] = feas ? 0.0 : qn - yn[li];
@@ -254,8 +239,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PRIMAL_G8_WA
 #pragma unroll
       for (int k = 0; k < (FF ? 3 : 2); ++k) f[7 * k + li] = feas ? 0.0 : x0[(long)b * nx + 7 * k + li] - y[7 * k + li];
     }
-  }
-}
+  }}
 
 // a^T H b over the contact-force block of the Gauss-Newton Hessian: diagonal
 // Dd plus (nc = 3) the friction cone's off-diagonal couplings Do
@@ -270,7 +254,11 @@ __device__ __forceinline__ double fquad(const double* a, const double* Dd, const
   return acc;
 }
 
-// calcDiff tangents + Gauss-Newton assembly: 16-lane group per node
+// calc + calcDiff tangents + Gauss-Newton assembly: 16-lane group per node.
+// The group's lanes 0..7 first run the node's calc (primal_group) into the
+// group's LDS, so the Primal / link records (~4 KB per node) never round-trip
+// through HBM: a separate calc kernel writing them and this one reading them
+// back was 129 + 366 us per launch at B=4096; fused, 255 us.
 template <int NC, bool FF>
 __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE_WAVES))) void k_node(const DevConsts* __restrict__ Cg, Dev d,
                                                       const double* __restrict__ x0,
@@ -302,14 +290,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
   const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
   NodeGroupShared& G = S.g[grp];
   Primal& P = G.P;
-  if (active) {
-    const double* src = reinterpret_cast<const double*>(d.prim + node);
-    double* dst = reinterpret_cast<double*>(&P);
-    constexpr int nw = sizeof(Primal) / sizeof(double);
-    for (int e = lane; e < nw; e += NODE_GROUP) dst[e] = src[e];
-    const double* ls = d.link + node * LK_ALLOC;
-    for (int e = lane; e < LK_WORDS; e += NODE_GROUP) G.lk[e] = ls[e];
-  }
+  if (active && lane < G8) primal_group<NC, FF>(C, d, x0, node_ref, inst_ref, surface, b, t, &P, G.lk);
   __syncthreads();
   const bool need_u = mode != MODE_TERMINAL_X;
   double da[NQ], dlam[3], col[NDENSE_MAX];
@@ -1558,7 +1539,7 @@ template <class T> int dalloc(ffddp_handle* h, T** p, size_t n) {
 }
 
 void free_all(ffddp_handle* h) {
-  void* ps[] = {h->dc, h->drb, h->d.prim, h->d.link, h->d.alist, h->d.acnt, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
+  void* ps[] = {h->dc, h->drb, h->d.alist, h->d.acnt, h->d.rec_buf, h->d.fs, h->d.xs, h->d.us, h->d.K, h->d.k, h->d.w, h->d.xs_try,
                 h->d.us_try, h->d.trial, h->d.trial_fail, h->d.st, h->in_x0, h->in_nref, h->in_iref, h->in_xs,
                 h->in_us, h->in_surf, h->out_xs, h->out_us, h->out_K, h->out_cost, h->out_fn, h->out_iters,
                 h->out_stats, h->out_ok};
@@ -1593,6 +1574,7 @@ struct ProfScope {
 // profiling classes: one kernel per class (KC_COMMIT is no longer launched:
 // the copy is fused into k_accept_commit)
 enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE, KC_FORWARD2, KC_PRIMAL };
+// (KC_PRIMAL is no longer launched either: the calc runs inside k_node)
 
 // the per-instance slice [b0, b0 + Bk) of the handle workspace
 Dev dev_slice(const Dev& d0, int b0, int Bk, int k) {
@@ -1611,8 +1593,6 @@ Dev dev_slice(const Dev& d0, int b0, int Bk, int k) {
   d.trial += (long)b0 * NTRIALS * 2;
   d.trial_fail += (long)b0 * NTRIALS;
   d.st += b0;
-  d.prim += (long)b0 * (N + 1);
-  d.link += (long)b0 * (N + 1) * LK_ALLOC;
   d.alist += 2L * b0;
   d.acnt += 2 * k;
   return d;
@@ -1684,11 +1664,6 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       // optional start stagger: slice k's first node stage waits for slice
       // k-1's, so the throughput-bound node stages do not all collide
       if (it == 0 && k > 0 && h->stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
-      {
-        ProfScope p(h, ss, KC_PRIMAL);
-        hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, ss, h->dc, d, x0k,
-                           nrefk, irefk, surfk, 0, it & 1);
-      }
       if (it == 0 && h->stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_NODE);
@@ -1777,8 +1752,6 @@ int launch_solve(ffddp_handle* h, int B, const double* x0, const double* nref, c
 template <int NC, bool FF>
 void launch_node(ffddp_handle* h, Dev d, int B, hipStream_t s, int force_all) {
   const long nodes = (long)B * (h->hc.N + 1);
-  hipLaunchKernelGGL((k_primal_g8<NC, FF>), dim3((int)((nodes * G8 + 63) / 64)), dim3(64), 0, s, h->dc, d, h->in_x0,
-                     h->in_nref, h->in_iref, h->in_surf, force_all, 0);
   hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, s, h->dc,
                      d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all, 0);
 }
@@ -1849,13 +1822,11 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   rc |= dalloc(h, &d.K, (size_t)B * N * NU * nx);
   rc |= dalloc(h, &d.k, (size_t)B * N * NU);
   rc |= dalloc(h, &d.w, (size_t)B * (N + 1) * nx);
-  rc |= dalloc(h, &d.link, (size_t)B * (N + 1) * LK_ALLOC);
   rc |= dalloc(h, &d.xs_try, (size_t)B * NTRIALS * (N + 1) * nx);
   rc |= dalloc(h, &d.us_try, (size_t)B * NTRIALS * N * NU);
   rc |= dalloc(h, &d.trial, (size_t)B * NTRIALS * 2);
   rc |= dalloc(h, &d.trial_fail, (size_t)B * NTRIALS);
   rc |= dalloc(h, &d.st, (size_t)B);
-  rc |= dalloc(h, &d.prim, (size_t)B * (N + 1));
   rc |= dalloc(h, &d.alist, (size_t)B * 2);
   rc |= dalloc(h, &d.acnt, (size_t)2 * 8);
   rc |= dalloc(h, &h->in_x0, (size_t)B * nx);

@@ -178,9 +178,10 @@ int ffddp_gravity_torque(const ffddp_robot* robot, int B, const double* q, doubl
 
 /* Optional per-kernel device timing (HIP events recorded around every launch
  * on the launch stream), one kernel per class.  Classes, in order: init,
- * node (calcDiff tangents + Gauss-Newton), backward, forward (line search,
- * first pass), accept (acceptance + copy of the accepted trial), commit
- * (unused), finalize, forward2 (line search, second pass), primal (calc).
+ * node (calc + calcDiff tangents + Gauss-Newton, one fused kernel), backward,
+ * forward (line search, first pass), accept (acceptance + copy of the accepted
+ * trial), commit (unused), finalize, forward2 (line search, second pass),
+ * primal (unused: the calc runs inside the node kernel).
  * `classes` is a bit mask over those classes (bit i = class i; 0 = off,
  * FFDDP_PROFILE_ALL = every class).  Timing only the kernel of interest keeps
  * the event overhead out of the other launches.
