@@ -650,8 +650,11 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
   return true;
 }
 
-template <bool FF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_WAVES))) void k_backward_w(const DevConsts* __restrict__ Cg, Dev d, int iter, int cur) {
+// LATE: the variant for the latency-bound iterations (few instances left, or
+// a small batch): phase C fully unrolled, 1 wave/SIMD register budget.
+template <bool FF, bool LATE = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (FF ? 2 : BW_WAVES)))) void k_backward_w(
+    const DevConsts* __restrict__ Cg, Dev d, int iter, int cur) {
   using S_t = BwW<FF>;
   constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
   constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane
@@ -690,6 +693,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
   S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
   // this lane's lower-triangle entries of Q (phase C) and V (phase F), fixed for the whole pass
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 63) / 64;
+  constexpr int QC_N = LATE ? NQL : QC_UNROLL;  // phase C unroll
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 63) / 64;
   int qrc[NQL], vij[NVL];
 #pragma unroll
@@ -814,7 +818,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FF ? 2 : BW_
       lds_sync();
       PP(2);
       // ---- phase C: Q lower triangle (mirrored), entries fixed per lane ----
-#pragma unroll QC_UNROLL
+#pragma unroll QC_N
       for (int k = 0; k < NQL; ++k) {
         if (l + 64 * k < NQE) {
           const int r = qrc[k] >> 8, c = qrc[k] & 255;
@@ -1506,6 +1510,8 @@ struct ffddp_handle {
   // instances are done the pass is latency-bound and 4 trials in one pass win
   std::vector<int> fw_sched{2, 2, 2, 2};
   int fw_late_it = 0;  // first iteration using the 1-wave/SIMD line-search variant (FFDDP_FW_LATE_IT)
+  int bw_late_it = 4;   // first iteration using the latency variant of the backward pass (FFDDP_BW_LATE_IT)
+  int bw_small_b = 256;  // slices of at most this many instances always use it (FFDDP_BW_SMALL_B)
   // optional per-kernel timing
   bool prof = false;
   int prof_mask = 0;
@@ -1673,7 +1679,10 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       if (it == 0 && h->stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_BACKWARD);
-        hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1);
+        if (it >= h->bw_late_it || Bk <= h->bw_small_b)
+          hipLaunchKernelGGL((k_backward_w<FF, true>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1);
+        else
+          hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1);
       }
       int n1 = NTRIALS;
       {
@@ -1795,6 +1804,8 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
       h->nstreams = v < 1 ? 1 : (v > 8 ? 8 : v);
     }
     if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
+    if (const char* bl = std::getenv("FFDDP_BW_LATE_IT")) h->bw_late_it = std::atoi(bl);
+    if (const char* bs = std::getenv("FFDDP_BW_SMALL_B")) h->bw_small_b = std::atoi(bs);
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
       h->fw_sched.clear();
       for (const char* p = fsch; *p;) {
