@@ -650,11 +650,14 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
   return true;
 }
 
-// LATE: the variant for the latency-bound iterations (few instances left, or
-// a small batch): phase C fully unrolled, 1 wave/SIMD register budget.
+// LATE: the variant for the latency-bound iterations (few instances left):
+// phase C fully unrolled, 1 wave/SIMD register budget.  Both variants are
+// launched every iteration; the device-side active count picks the one that
+// works (late_max: the most active instances the LATE variant takes, so its
+// waves fit one per SIMD), the other one's blocks exit at once.
 template <bool FF, bool LATE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (FF ? 2 : BW_WAVES)))) void k_backward_w(
-    const DevConsts* __restrict__ Cg, Dev d, int iter, int cur) {
+    const DevConsts* __restrict__ Cg, Dev d, int iter, int cur, int late_max) {
   using S_t = BwW<FF>;
   constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
   constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane
@@ -663,7 +666,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   const int l = threadIdx.x;
   if (blockIdx.x == 0 && l == 0) d.acnt[cur ^ 1] = 0;  // the list k_accept_commit builds
   const ActiveList al = active_list(d, cur);
-  if ((int)blockIdx.x >= al.n) return;
+  if ((int)blockIdx.x >= al.n || (LATE ? al.n > late_max : al.n <= late_max)) return;
   const int b = al.list[blockIdx.x];
   InstState* st = d.st + b;
   if (st->done) return;
@@ -1510,8 +1513,9 @@ struct ffddp_handle {
   // instances are done the pass is latency-bound and 4 trials in one pass win
   std::vector<int> fw_sched{2, 2, 2, 2};
   int fw_late_it = 0;  // first iteration using the 1-wave/SIMD line-search variant (FFDDP_FW_LATE_IT)
-  int bw_late_it = 4;   // first iteration using the latency variant of the backward pass (FFDDP_BW_LATE_IT)
-  int bw_small_b = 256;  // slices of at most this many instances always use it (FFDDP_BW_SMALL_B)
+  int bw_late_max = -1;  // active instances up to which a slice's backward pass uses the latency variant
+                         // (FFDDP_BW_LATE_MAX; -1: SIMDs / slices)
+  int n_simd = 1024;     // SIMDs of the device (4 per CU)
   // optional per-kernel timing
   bool prof = false;
   int prof_mask = 0;
@@ -1679,10 +1683,11 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       if (it == 0 && h->stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_BACKWARD);
-        if (it >= h->bw_late_it || Bk <= h->bw_small_b)
-          hipLaunchKernelGGL((k_backward_w<FF, true>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1);
-        else
-          hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1);
+        const int lmax = h->bw_late_max >= 0 ? h->bw_late_max : h->n_simd / S;
+        if (lmax < Bk) hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1, lmax);
+        if (lmax > 0)
+          hipLaunchKernelGGL((k_backward_w<FF, true>), dim3(lmax < Bk ? lmax : Bk), dim3(64), 0, ss, h->dc, d, it, it & 1,
+                             lmax);
       }
       int n1 = NTRIALS;
       {
@@ -1798,14 +1803,16 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     return FFDDP_E_INVALID;
   }
   {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
+      h->n_simd = 4 * cu;
     const char* ns = std::getenv("FFDDP_STREAMS");
     if (ns) {
       const int v = std::atoi(ns);
       h->nstreams = v < 1 ? 1 : (v > 8 ? 8 : v);
     }
     if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
-    if (const char* bl = std::getenv("FFDDP_BW_LATE_IT")) h->bw_late_it = std::atoi(bl);
-    if (const char* bs = std::getenv("FFDDP_BW_SMALL_B")) h->bw_small_b = std::atoi(bs);
+    if (const char* bl = std::getenv("FFDDP_BW_LATE_MAX")) h->bw_late_max = std::atoi(bl);
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
       h->fw_sched.clear();
       for (const char* p = fsch; *p;) {
