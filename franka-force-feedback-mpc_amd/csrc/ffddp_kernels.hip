@@ -1516,6 +1516,7 @@ struct ffddp_handle {
   int bw_late_max = -1;  // active instances up to which a slice's backward pass uses the latency variant
                          // (FFDDP_BW_LATE_MAX; -1: SIMDs / slices)
   int n_simd = 1024;     // SIMDs of the device (4 per CU)
+  bool fw_fill = true;   // widen the first line-search pass to fill the SIMDs (FFDDP_FW_FILL=0: off)
   // optional per-kernel timing
   bool prof = false;
   int prof_mask = 0;
@@ -1695,6 +1696,10 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
         // fw_first; the second pass evaluates the rest for the instances that
         // accepted none of them
         n1 = it < (int)h->fw_sched.size() ? h->fw_sched[it] : h->fw_first;
+        // a small batch leaves SIMDs idle: evaluate as many step lengths in
+        // the first pass as one wave per SIMD holds (8 groups per wave), so
+        // the second pass (a whole extra rollout on the chain) is rarely needed
+        if (h->fw_fill) n1 = std::max(n1, std::min(NTRIALS, 8 * h->n_simd / std::max(B, 1)));
         const bool late = it >= h->fw_late_it;
         auto fw = [&](int tr0, int ntr, int more) {
           const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
@@ -1813,6 +1818,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     }
     if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
     if (const char* bl = std::getenv("FFDDP_BW_LATE_MAX")) h->bw_late_max = std::atoi(bl);
+    if (const char* ff = std::getenv("FFDDP_FW_FILL")) h->fw_fill = std::atoi(ff) != 0;
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
       h->fw_sched.clear();
       for (const char* p = fsch; *p;) {
