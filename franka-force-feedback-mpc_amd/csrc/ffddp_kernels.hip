@@ -1304,8 +1304,25 @@ __global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restric
   const double* su = d.us_try + ((long)b * NTRIALS + acc) * perU;
   double* dx = d.xs + (long)b * perX;
   double* du = d.us + (long)b * perU;
-  for (long i = l; i < perX; i += 16) dx[i] = sx[i];
-  for (long i = l; i < perU; i += 16) du[i] = su[i];
+  // all loads of a chunk in flight before its stores (a plain element loop
+  // made each lane wait for one load at a time)
+  constexpr int CH = 16;
+  for (long base = l; base < perX + perU; base += 16 * CH) {
+    double v[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const long i = base + 16 * u;
+      v[u] = i < perX ? sx[i] : (i < perX + perU ? su[i - perX] : 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const long i = base + 16 * u;
+      if (i < perX)
+        dx[i] = v[u];
+      else if (i < perX + perU)
+        du[i - perX] = v[u];
+    }
+  }
 }
 
 // solution read-back helpers: iter/ok, contact force at knots 0 and 1
