@@ -565,25 +565,37 @@ __device__ __forceinline__ double chol_solve_rows(const double (&Lr)[NU], double
   return out;
 }
 
-// crocoddyl::BoxQP::solve with variable i on lane i (see boxqp_reg for the
-// algorithm).  hrow = row i of H; x in = warm start, out = solution; Lr = rows
-// of the masked factor of the final free set; clmask = final clamped set.
+// sum / max over lanes 0..7 (lanes >= NU hold 0): DPP inside the first 8
+// lanes, the result read back from lane 0 (wave-uniform)
+__device__ __forceinline__ double sum8_u(double v) { return bcast(g8_sum(v), 0); }
+__device__ __forceinline__ double max8_u(double v) {
+  v = fmax(v, dpp64<0x141>(v));  // row_half_mirror
+  v = fmax(v, dpp64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmax(v, dpp64<0x4E>(v));   // quad_perm [2,3,0,1]
+  return bcast(v, 0);
+}
+
+// crocoddyl::BoxQP::solve with variable i on lane i: projected Newton on the
+// free set, refactored when it changes, Armijo line search over the same
+// alphas.  hrow = row i of H; x in = warm start, out = solution; Lr = rows of
+// the masked factor of the final free set; clmask = final clamped set.  The
+// scalar products (objective values, directional derivative) and the step
+// norm are lane-local terms summed / maxed by DPP over the 8 lanes; only the
+// vectors a mat-vec needs (x, the trial point) are broadcast.
 __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&hrow)[NU], double q, double lb,
                                             double ub, double& x, double (&Lr)[NU], int& clmask, int lane) {
   x = fmax(fmin(x, ub), lb);
   bool have = false, cl = false;
   double xsf = 0.0;
-  double qb[NU];
-#pragma unroll
-  for (int j = 0; j < NU; ++j) qb[j] = bcast(q, j);
 #pragma unroll 1
   for (int it = 0; it < C.qp_maxiter; ++it) {
     double xb[NU];
 #pragma unroll
     for (int j = 0; j < NU; ++j) xb[j] = bcast(x, j);
-    double g = q;
+    double hx = 0.0;
 #pragma unroll
-    for (int j = 0; j < NU; ++j) g += hrow[j] * xb[j];
+    for (int j = 0; j < NU; ++j) hx += hrow[j] * xb[j];
+    const double g = q + hx;
     const bool c = (x == lb && g > 0.0) || (x == ub && g < 0.0);
     const bool changed = !have || ((__ballot(c != cl) & 0x7Full) != 0);
     cl = c;
@@ -604,44 +616,18 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
       clmask = m;
     }
     const double dx = cl ? 0.0 : xsf - x;
-    double dmax = 0.0;
-#pragma unroll
-    for (int j = 0; j < NU; ++j) dmax = fmax(dmax, fabs(bcast(dx, j)));
-    if (dmax < C.qp_th_grad) break;
-    double gb[NU];
-#pragma unroll
-    for (int j = 0; j < NU; ++j) gb[j] = bcast(g, j);
-    double fold;
-    {
-      double hx = 0.0;
-#pragma unroll
-      for (int j = 0; j < NU; ++j) hx += hrow[j] * xb[j];
-      double a1 = 0.0, a2 = 0.0;
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        a1 += xb[i] * bcast(hx, i);
-        a2 += qb[i] * xb[i];
-      }
-      fold = 0.5 * a1 + a2;
-    }
+    if (max8_u(fabs(dx)) < C.qp_th_grad) break;
+    const double fold = sum8_u(0.5 * x * hx + q * x);
 #pragma unroll 1
     for (int ia = 0; ia < NTRIALS; ++ia) {
       const double al = C.alphas[ia];
       const double xn = fmax(fmin(x + al * dx, ub), lb);
-      double xnb[NU];
-#pragma unroll
-      for (int j = 0; j < NU; ++j) xnb[j] = bcast(xn, j);
       double hxn = 0.0;
 #pragma unroll
-      for (int j = 0; j < NU; ++j) hxn += hrow[j] * xnb[j];
-      double a1 = 0.0, a2 = 0.0, gd = 0.0;
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        a1 += xnb[i] * bcast(hxn, i);
-        a2 += qb[i] * xnb[i];
-        gd += gb[i] * (xb[i] - xnb[i]);
-      }
-      if (fold - (0.5 * a1 + a2) > C.qp_th_acceptstep * gd) {
+      for (int j = 0; j < NU; ++j) hxn += hrow[j] * bcast(xn, j);
+      const double fnew = sum8_u(0.5 * xn * hxn + q * xn);
+      const double gd = sum8_u(g * (x - xn));
+      if (fold - fnew > C.qp_th_acceptstep * gd) {
         x = xn;
         break;
       }
