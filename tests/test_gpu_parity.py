@@ -228,3 +228,25 @@ def test_gravity_torque_dev_matches_oracle():
     err = rel_err(td.cpu().numpy(), P.gravity_torque(q))
     log_parity("gravity_dev", err=err)
     assert err < 1e-12
+
+
+# Launch-schedule variants (the small parity batches otherwise always take
+# the latency variant of the backward pass and a single 10-step-length line
+# search pass): the same solves through the 2-waves/SIMD backward variant and
+# through the two-pass line search (2 step lengths first, the rest second).
+@pytest.mark.parametrize("env", [{"FFDDP_BW_LATE_MAX": "0"}, {"FFDDP_FW_FILL": "0"},
+                                 {"FFDDP_BW_LATE_MAX": "0", "FFDDP_FW_FILL": "0", "FFDDP_FW_FIRST": "2"}])
+@pytest.mark.parametrize("variant", ["classical", "ff"])
+def test_solve_schedule_variants(variant, env, monkeypatch):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)  # read by ffddp_create
+    N, B = 30, 4
+    cfg = _cfg(variant, N, "normal_1d")
+    b = make_batch(variant, B, N, seed=22, surface=1)
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B))
+    tag = "/".join(f"{k}={v}" for k, v in env.items())
+    _check_solves(f"solve/schedule/{variant}/{tag}", cfg, b, solver, ref)
+    if "FFDDP_FW_FILL" in env:
+        assert np.any(solver.stats[:, 7] > 0) or np.all(solver.stats[:, 6] > 0)
