@@ -739,8 +739,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         }
         S.Vx[l] = vx;
       }
-      dg += wave_sum(cdg);
-      dq += wave_sum(cdq);
+      dg += cdg;  // lane-local; summed over the wave after the node loop
+      dq += cdq;
     }
     lds_sync();
     for (int t = N - 1; t >= 0; --t) {
@@ -954,9 +954,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         S.Vx[l] = vx;  // old Vx is dead after phase B
       }
       badv = __any(badv);
-      cdg = wave_sum(cdg);
-      cdq = wave_sum(cdq);
-      cst = wave_sum(cst);
       if (badv) {
         failed = true;
         break;
@@ -968,7 +965,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       PP(7);
     }
     // ---- retry bookkeeping (SolverFDDP::solve: increaseRegularization) ----
-    if (!failed) break;
+    if (!failed) {
+      // expected-improvement terms: lane-local sums over the nodes, reduced
+      // once here instead of three wave reductions per node
+      dg = wave_sum(dg);
+      dq = wave_sum(dq);
+      stop = wave_sum(stop);
+      break;
+    }
     retries++;
     preg = fmin(preg * C.reg_inc, C.reg_max);
     if (preg == C.reg_max) {
