@@ -759,7 +759,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         pkp = d.k[((long)b * N + tn) * NU + lu];
         pus = d.us[((long)b * N + tn) * NU + lu];
       }
-      lds_sync();
+      // no barrier here: phase A reads only V / Vx, and its closing barrier
+      // publishes the staged record and gap before phase B reads them
       PP(0);
       const double* Ar = S.R + rec_off_A();
       // ---- phase A: W = V D (NX x 7), Y = D' V D (7 x 7), z = D' Vx ----
