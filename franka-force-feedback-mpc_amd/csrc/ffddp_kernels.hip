@@ -1512,7 +1512,8 @@ struct ffddp_handle {
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
   std::vector<hipEvent_t> stg;  // start-stagger events (FFDDP_STAGGER)
   bool caller_slice = true;  // FFDDP_CALLER_SLICE
-  int stagger = 2;  // 0 off, 1 after the previous slice's node stage, 2 after its primal kernel
+  int stagger = 2;  // 0 off, 1 after the previous slice's first node stage, 2 after its init (the calc is
+                    // fused into k_node, so there is no earlier boundary; 0 / 1 / 2 measure alike)
   int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
   // first-pass trial counts of the first iterations (FFDDP_FW_SCHED="2,2,2,2"):
   // while every instance is active the line search is throughput-bound, so a
