@@ -17,8 +17,10 @@
 //   k_forward_g8  line search: one 8-lane group per (instance, step length) —
 //               the trials of SolverFDDP::solve evaluated concurrently (the
 //               first accepted one is the sequential answer).
-//   k_accept_commit  acceptance test / regularisation / stopping
-//               (SolverFDDP::solve) and the copy of the accepted trial into (xs, us).
+//   k_accept    acceptance test / regularisation / stopping (SolverFDDP::solve),
+//               one lane per instance; the accepted trial stays in place (the
+//               next k_node reads it and writes it into xs / us; k_commit at
+//               the end of the solve for the rest).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -89,7 +91,7 @@ struct Dev {
 // the rest exit at once.  Without it a late iteration's few active
 // instances are scattered over the whole grid, and a grid larger than one
 // wave per SIMD (the 1-wave/SIMD line search with 4 trials) ran its active
-// waves in two dispatch rounds.  k_accept_commit appends the instances that
+// waves in two dispatch rounds.  k_accept appends the instances that
 // continue to the other list; k_backward_w zeroes that list's length first.
 struct ActiveList {
   const int* list;
@@ -170,7 +172,8 @@ template <int NC, bool FF>
 __device__ __forceinline__ void primal_group(const DevConsts& C, const Dev& d, const double* __restrict__ x0,
                                              const double* __restrict__ node_ref, const double* __restrict__ inst_ref,
                                              const uint8_t* __restrict__ surface, int b, int t, Primal* P,
-                                             double* lk) {
+                                             double* lk, const double* __restrict__ xsrc,
+                                             const double* __restrict__ usrc) {
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
   const int li = g8_lane();
@@ -179,12 +182,20 @@ __device__ __forceinline__ void primal_group(const DevConsts& C, const Dev& d, c
   const bool surf = surface[b] != 0;
   const bool terminal = t == N;
   const int mode = !terminal ? MODE_RUNNING : (FF ? MODE_TERMINAL_U : MODE_TERMINAL_X);
-  const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
+  const double* y = xsrc + (long)t * nx;
   const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
   const double* xreg = inst_ref + (long)b * 21;
-  const double* uin = FF ? (y + 14) : (terminal ? nullptr : d.us + ((long)b * N + t) * NU);
+  const double* uin = FF ? (y + 14) : (terminal ? nullptr : usrc + (long)t * NU);
   const double q = y[ji], v = y[7 + ji];
   const double u = (uin != nullptr) ? uin[ji] : 0.0;
+  // setCandidate: the accepted line-search trial becomes (xs, us) here, node
+  // by node, instead of a whole-trajectory copy on the iteration's chain
+  const double* xdst = d.xs + (long)b * (N + 1) * nx;
+  if (J && xsrc != xdst) {
+#pragma unroll
+    for (int k = 0; k < (FF ? 3 : 2); ++k) d.xs[((long)b * (N + 1) + t) * nx + 7 * k + li] = y[7 * k + li];
+    if (!terminal) d.us[((long)b * N + t) * NU + li] = usrc[(long)t * NU + li];
+  }
   double lam[3];
   const double pc = node_primal_g8<NC>(C, mode, surf, q, v, u, xreg[ji], xreg[7 + ji], xreg[14 + ji], ref,
                                        P, lk, lam);
@@ -204,7 +215,7 @@ __device__ __forceinline__ void primal_group(const DevConsts& C, const Dev& d, c
         part += 0.5 * C.w_y * a_;
       }
       if (!terminal) {
-        const double ww = d.us[((long)b * N + t) * NU + li];
+        const double ww = usrc[(long)t * NU + li];
         if (C.w_w > 0.0) part += 0.5 * C.w_w * (ww * ww);
         if (C.w_ws > 0.0) {
           const double ov = fabs(ww) - C.ws_lim[li];
@@ -225,14 +236,14 @@ __device__ __forceinline__ void primal_group(const DevConsts& C, const Dev& d, c
   if (J) {
     if (!terminal) {
       double* f = d.fs + ((long)b * (N + 1) + t + 1) * nx;
-      const double* yn = d.xs + ((long)b * (N + 1) + t + 1) * nx;
+      const double* yn = xsrc + (long)(t + 1) * nx;
       const double dt = C.dt;
       const double a = P->a[li];  // this lane's own store
       const double qn = (mode == MODE_TERMINAL_X) ? q : q + (v * dt + a * dt * dt);
       const double vn = (mode == MODE_TERMINAL_X) ? v : v + a * dt;
       f[li] = feas ? 0.0 : qn - yn[li];
       f[7 + li] = feas ? 0.0 : vn - yn[7 + li];
-      if (FF) f[14 + li] = feas ? 0.0 : (C.alpha * y[14 + li] + C.beta * d.us[((long)b * N + t) * NU + li]) - yn[14 + li];
+      if (FF) f[14 + li] = feas ? 0.0 : (C.alpha * y[14 + li] + C.beta * usrc[(long)t * NU + li]) - yn[14 + li];
     }
     if (t == 0) {
       double* f = d.fs + (long)b * (N + 1) * nx;
@@ -286,11 +297,17 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
   const bool terminal = t == N;
   constexpr bool ff = FF;
   const int mode = !terminal ? MODE_RUNNING : (ff ? MODE_TERMINAL_U : MODE_TERMINAL_X);
-  const double* y = d.xs + ((long)b * (N + 1) + t) * nx;
+  // current iterate: the trial the last line search accepted (not yet copied
+  // into xs / us: primal_group does that for its node), else xs / us
+  const long perX = (long)(N + 1) * nx, perU = (long)N * NU;
+  const int acc = active ? d.st[b].accepted : -1;
+  const double* xsrc = acc >= 0 ? d.xs_try + ((long)b * NTRIALS + acc) * perX : d.xs + (long)b * perX;
+  const double* usrc = acc >= 0 ? d.us_try + ((long)b * NTRIALS + acc) * perU : d.us + (long)b * perU;
+  const double* y = xsrc + (long)t * nx;
   const double* ref = node_ref + ((long)b * (N + 1) + t) * 6;
   NodeGroupShared& G = S.g[grp];
   Primal& P = G.P;
-  if (active && lane < G8) primal_group<NC, FF>(C, d, x0, node_ref, inst_ref, surface, b, t, &P, G.lk);
+  if (active && lane < G8) primal_group<NC, FF>(C, d, x0, node_ref, inst_ref, surface, b, t, &P, G.lk, xsrc, usrc);
   __syncthreads();
   const bool need_u = mode != MODE_TERMINAL_X;
   double da[NQ], dlam[3], col[NDENSE_MAX];
@@ -377,7 +394,7 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
         rec[rec_off_Lx(nx) + 14 + kk] = lu + C.w_y * C.Wy2[14 + kk] * (y[14 + kk] - x0[(long)b * nx + 14 + kk]);
         // augmented control terms: Lu = w_w w + w_s g_soft ; Luu = diag ; Lxu = 0
         double wk = 0.0;
-        if (!terminal) wk = d.us[((long)b * N + t) * NU + kk];
+        if (!terminal) wk = usrc[(long)t * NU + kk];
         const double ov = fabs(wk) - C.ws_lim[kk];
         const bool act = ov > 0.0;
         const double gs = act ? ov * (wk > 0.0 ? 1.0 : (wk < 0.0 ? -1.0 : 0.0)) : 0.0;
@@ -650,7 +667,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   const DevConsts& C = *Cg;
   const int N = C.N;
   const int l = threadIdx.x;
-  if (blockIdx.x == 0 && l == 0) d.acnt[cur ^ 1] = 0;  // the list k_accept_commit builds
+  if (blockIdx.x == 0 && l == 0) d.acnt[cur ^ 1] = 0;  // the list k_accept builds
   const ActiveList al = active_list(d, cur);
   if ((int)blockIdx.x >= al.n || (LATE ? al.n > late_max : al.n <= late_max)) return;
   const int b = al.list[blockIdx.x];
@@ -1253,41 +1270,40 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int 
   return acc;
 }
 
-// acceptance + setCandidate copy of the accepted trial into (xs, us):
-// ACC_IPB instances per 64-lane block, a 16-lane quarter each (its lane 0
-// decides, the quarter copies); the block appends its continuing instances to
-// the next active list with ONE atomic (one atomic per instance made the
-// 4096-instance launch 3x slower; 256-thread blocks instead waited for free
-// CU slots behind the other slices' node kernels)
-constexpr int ACC_IPB = 4;
-__global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1,
-                                                      int cur) {
+// acceptance / regularisation / stopping, one lane per instance; the
+// continuing instances are appended to the next active list with one atomic
+// per wave.  The accepted trial is not copied here: the next iteration's
+// k_node reads it in place and writes it into (xs, us) node by node, and
+// k_commit does it for the instances no further k_node visits.
+__global__ __launch_bounds__(64) void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1, int cur) {
   const DevConsts& C = *Cg;
   const ActiveList al = active_list(d, cur);
-  const int q = threadIdx.x / 16, l = threadIdx.x % 16;
-  const int slot = (int)blockIdx.x * ACC_IPB + q;
-  if ((int)blockIdx.x * ACC_IPB >= al.n) return;
+  if ((int)blockIdx.x * 64 >= al.n) return;
+  const int slot = (int)blockIdx.x * 64 + (int)threadIdx.x;
   const bool has = slot < al.n;
   const int b = has ? al.list[slot] : 0;
-  __shared__ int acc_s[ACC_IPB], cont_s[ACC_IPB];
-  if (l == 0) {
-    acc_s[q] = has ? accept_instance(C, d, b, iter, n1) : -1;
-    cont_s[q] = (has && !d.st[b].done) ? 1 : 0;
+  bool cont = false;
+  if (has) {
+    accept_instance(C, d, b, iter, n1);
+    cont = d.st[b].done == 0;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int n = 0;
-#pragma unroll
-    for (int i = 0; i < ACC_IPB; ++i) n += cont_s[i];
-    if (n > 0) {
-      int pos = atomicAdd(d.acnt + (cur ^ 1), n);
-      int* next = d.alist + (long)(cur ^ 1) * d.B;
-#pragma unroll
-      for (int i = 0; i < ACC_IPB; ++i)
-        if (cont_s[i]) next[pos++] = al.list[(int)blockIdx.x * ACC_IPB + i];
-    }
-  }
-  const int acc = acc_s[q];
+  const unsigned long long m = __ballot(cont);
+  int base = 0;
+  if (threadIdx.x == 0 && m != 0ull) base = atomicAdd(d.acnt + (cur ^ 1), __popcll(m));
+  base = __builtin_amdgcn_readfirstlane(base);
+  if (cont) d.alist[(long)(cur ^ 1) * d.B + base + __popcll(m & ((1ull << threadIdx.x) - 1ull))] = b;
+}
+
+// end of solve: the accepted trial of every instance whose last iteration
+// accepted one and that no k_node visited since becomes (xs, us); 16 lanes
+// per instance, a chunk's loads all in flight before its stores
+constexpr int COMMIT_IPB = 4;
+__global__ __launch_bounds__(64) void k_commit(const DevConsts* __restrict__ Cg, Dev d) {
+  const DevConsts& C = *Cg;
+  const int q = threadIdx.x / 16, l = threadIdx.x % 16;
+  const int b = (int)blockIdx.x * COMMIT_IPB + q;
+  if (b >= d.B) return;
+  const int acc = d.st[b].accepted;
   if (acc < 0) return;
   const int N = C.N, nx = C.nx;
   const long perX = (long)(N + 1) * nx, perU = (long)N * NU;
@@ -1295,8 +1311,6 @@ __global__ __launch_bounds__(64) void k_accept_commit(const DevConsts* __restric
   const double* su = d.us_try + ((long)b * NTRIALS + acc) * perU;
   double* dx = d.xs + (long)b * perX;
   double* du = d.us + (long)b * perU;
-  // all loads of a chunk in flight before its stores (a plain element loop
-  // made each lane wait for one load at a time)
   constexpr int CH = 16;
   for (long base = l; base < perX + perU; base += 16 * CH) {
     double v[CH];
@@ -1591,10 +1605,9 @@ struct ProfScope {
   }
 };
 
-// profiling classes: one kernel per class (KC_COMMIT is no longer launched:
-// the copy is fused into k_accept_commit)
+// profiling classes: one kernel per class (KC_COMMIT: the end-of-solve
+// k_commit; KC_PRIMAL is no longer launched: the calc runs inside k_node)
 enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE, KC_FORWARD2, KC_PRIMAL };
-// (KC_PRIMAL is no longer launched either: the calc runs inside k_node)
 
 // the per-instance slice [b0, b0 + Bk) of the handle workspace
 Dev dev_slice(const Dev& d0, int b0, int Bk, int k) {
@@ -1730,8 +1743,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       }
       {
         ProfScope p(h, ss, KC_ACCEPT);
-        hipLaunchKernelGGL(k_accept_commit, dim3((Bk + ACC_IPB - 1) / ACC_IPB), dim3(64), 0, ss, h->dc, d, it, n1,
-                           it & 1);
+        hipLaunchKernelGGL(k_accept, dim3((Bk + 63) / 64), dim3(64), 0, ss, h->dc, d, it, n1, it & 1);
       }
     }
   }
@@ -1743,6 +1755,10 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
     const hipStream_t ss = sl[k].s;
     const long b0 = sl[k].b0;
     const int Bk = sl[k].B;
+    {
+      ProfScope p(h, ss, KC_COMMIT);
+      hipLaunchKernelGGL(k_commit, dim3((Bk + COMMIT_IPB - 1) / COMMIT_IPB), dim3(64), 0, ss, h->dc, d);
+    }
     {
       ProfScope p(h, ss, KC_FINALIZE);
       hipLaunchKernelGGL((k_finalize<NC, FF>), dim3((2 * Bk + 63) / 64), dim3(64), 0, ss, h->dc, d, maxiter,
