@@ -538,6 +538,27 @@ __device__ __forceinline__ double bcast(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
+// lane k's value to every lane of its 16-lane row (DPP row_newbcast: one
+// v_mov_b64_dpp, no SGPR round trip).  The 7x7 algebra below lives on lanes
+// 0..6 of row 0; the other rows compute on their own (unused) lanes.
+template <int K> __device__ __forceinline__ double rowb_(double v) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const long long r = __builtin_amdgcn_update_dpp(x, x, 0x150 + K, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, r);
+}
+// k is a constant after unrolling: the switch folds away
+__device__ __forceinline__ double rowb(double v, int k) {
+  switch (k) {
+    case 0: return rowb_<0>(v);
+    case 1: return rowb_<1>(v);
+    case 2: return rowb_<2>(v);
+    case 3: return rowb_<3>(v);
+    case 4: return rowb_<4>(v);
+    case 5: return rowb_<5>(v);
+    default: return rowb_<6>(v);
+  }
+}
+
 // In-place LLT of the SPD matrix whose row i is held by lane i: on exit
 // a[j] (j < i) = L_ij and a[i] = 1 / L_ii (same operation order as
 // chol_packed).  Returns false (uniformly) at the first non-positive pivot.
@@ -547,12 +568,12 @@ __device__ __forceinline__ bool chol_rows(double (&a)[NU], int lane) {
     double d = a[k];
 #pragma unroll
     for (int m = 0; m < k; ++m) d -= a[m] * a[m];
-    const double dk = bcast(d, k);
-    if (!(dk > 0.0)) return false;
+    const double dk = rowb(d, k);
+    if (__ballot(!(dk > 0.0)) & 1ull) return false;  // lane 0 holds row 0's pivot
     const double il = rsqrt_nr(dk);
     double s = a[k];
 #pragma unroll
-    for (int m = 0; m < k; ++m) s -= a[m] * bcast(a[m], k);
+    for (int m = 0; m < k; ++m) s -= a[m] * rowb(a[m], k);
     a[k] = (lane == k) ? il : ((lane > k) ? s * il : a[k]);
   }
   return true;
@@ -566,15 +587,15 @@ __device__ __forceinline__ double chol_solve_rows(const double (&Lr)[NU], double
     double s = r;
 #pragma unroll
     for (int m = 0; m < k; ++m) s -= Lr[m] * y[m];
-    y[k] = bcast(s * Lr[k], k);
+    y[k] = rowb(s * Lr[k], k);
   }
   double x[NU];
 #pragma unroll
   for (int k = NU - 1; k >= 0; --k) {
     double s = y[k];
 #pragma unroll
-    for (int m = k + 1; m < NU; ++m) s -= bcast(Lr[k], m) * x[m];
-    x[k] = s * bcast(Lr[k], k);
+    for (int m = k + 1; m < NU; ++m) s -= rowb(Lr[k], m) * x[m];
+    x[k] = s * rowb(Lr[k], k);
   }
   double out = 0.0;
 #pragma unroll
@@ -608,7 +629,7 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
   for (int it = 0; it < C.qp_maxiter; ++it) {
     double xb[NU];
 #pragma unroll
-    for (int j = 0; j < NU; ++j) xb[j] = bcast(x, j);
+    for (int j = 0; j < NU; ++j) xb[j] = rowb(x, j);
     double hx = 0.0;
 #pragma unroll
     for (int j = 0; j < NU; ++j) hx += hrow[j] * xb[j];
@@ -641,7 +662,7 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
       const double xn = fmax(fmin(x + al * dx, ub), lb);
       double hxn = 0.0;
 #pragma unroll
-      for (int j = 0; j < NU; ++j) hxn += hrow[j] * bcast(xn, j);
+      for (int j = 0; j < NU; ++j) hxn += hrow[j] * rowb(xn, j);
       const double fnew = sum8_u(0.5 * xn * hxn + q * xn);
       const double gd = sum8_u(g * (x - xn));
       if (fold - fnew > C.qp_th_acceptstep * gd) {
