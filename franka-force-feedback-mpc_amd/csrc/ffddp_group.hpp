@@ -27,8 +27,8 @@ __device__ __forceinline__ int g8_lane() { return (int)(threadIdx.x & 7); }
 // Cross-lane moves inside the 8-lane group without going through LDS:
 // DPP row_shr / row_shl for the scans (groups are 8-aligned inside 16-lane
 // DPP rows; lanes whose source falls outside the group are masked by the
-// callers), ds_swizzle BROADCAST(8, k) for broadcasts, DPP half-mirror and
-// quad permutes for the sums.
+// callers), DPP row_newbcast for broadcasts, DPP half-mirror and quad
+// permutes for the sums.
 // bound_ctrl: a lane whose source is outside the row reads 0 (what the scans
 // need), and no "old" operand has to be zeroed first: one v_mov_b32_dpp per
 // 32-bit half and nothing else (with update_dpp(0, ...) every move also cost
@@ -43,15 +43,26 @@ template <int CTRL> __device__ __forceinline__ int dpp32(int v) {
   return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true);
 }
 #ifndef G8_DPP
-#define G8_DPP 0
+#define G8_DPP 2
 #endif
-// Broadcast of group lane K.  ds_swizzle BROADCAST(8, K) by default; with
-// G8_DPP two DPP moves instead (quad_perm [k,k,k,k] gives every quad its lane
-// K & 3, then the quad of the group that does not hold lane K takes the
-// other quad's value by row_shr:4 / row_shl:4 under a bank mask; groups are
-// 8-aligned inside 16-lane DPP rows).  Measured: no faster.
+// Broadcast of group lane K.  Default (G8_DPP 2): row_newbcast of lane K and
+// of lane 8 + K (one v_mov_b64_dpp each: both 8-lane groups of the 16-lane
+// DPP row), each group keeping its own; 2-3 % faster line search than
+// ds_swizzle BROADCAST(8, K) (G8_DPP 0), which goes through the LDS pipe.
+// G8_DPP 1: quad_perm [k,k,k,k] then row_shr:4 / row_shl:4 under a bank
+// mask (four 32-bit DPP moves; no faster than the swizzle).
+template <int K> __device__ __forceinline__ double g8_rowb(double v) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const long long r = __builtin_amdgcn_update_dpp(x, x, 0x150 + K, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, r);
+}
 template <int K> __device__ __forceinline__ double g8_bc(double v) {
-#if G8_DPP
+#if G8_DPP == 2
+  // both groups of the 16-lane DPP row: row_newbcast of lane K and of lane
+  // 8 + K (one v_mov_b64_dpp each), then each group keeps its own
+  const double a = g8_rowb<K>(v), b = g8_rowb<8 + K>(v);
+  return (threadIdx.x & 8) ? b : a;
+#elif G8_DPP
   constexpr int qp = (K & 3) * 0x55;
   constexpr int sh = K < 4 ? 0x114 : 0x104;
   constexpr int bm = K < 4 ? 0xA : 0x5;
@@ -67,7 +78,21 @@ template <int K> __device__ __forceinline__ double g8_bc(double v) {
   return __hiloint2double(hi, lo);
 #endif
 }
-__device__ __forceinline__ double g8_get(double v, int src) {
+// ROW: the group is lanes 0..7 of a 16-lane DPP row whose lanes 8..15 do
+// not take part (k_node's calc): one row_newbcast move per broadcast
+template <bool ROW = false> __device__ __forceinline__ double g8_get(double v, int src) {
+  if (ROW) {
+    switch (src) {
+      case 0: return g8_rowb<0>(v);
+      case 1: return g8_rowb<1>(v);
+      case 2: return g8_rowb<2>(v);
+      case 3: return g8_rowb<3>(v);
+      case 4: return g8_rowb<4>(v);
+      case 5: return g8_rowb<5>(v);
+      case 6: return g8_rowb<6>(v);
+      default: return g8_rowb<7>(v);
+    }
+  }
   switch (src) {
     case 0: return g8_bc<0>(v);
     case 1: return g8_bc<1>(v);
@@ -99,29 +124,29 @@ __device__ __forceinline__ int g8_or(int v) {
 }
 
 // LLT with row i on group lane i (lanes 0..6); reciprocal diagonal as in chol_packed
-__device__ __forceinline__ void g8_chol_rows(double (&a)[NQ], int li) {
+template <bool ROW = false> __device__ __forceinline__ void g8_chol_rows(double (&a)[NQ], int li) {
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
     double d = a[k];
 #pragma unroll
     for (int m = 0; m < k; ++m) d -= a[m] * a[m];
-    const double il = rsqrt_nr(g8_get(d, k));
+    const double il = rsqrt_nr(g8_get<ROW>(d, k));
     double s = a[k];
 #pragma unroll
-    for (int m = 0; m < k; ++m) s -= a[m] * g8_get(a[m], k);
+    for (int m = 0; m < k; ++m) s -= a[m] * g8_get<ROW>(a[m], k);
     a[k] = (li == k) ? il : ((li > k) ? s * il : a[k]);
   }
 }
 
 // forward substitution L y = r (row layout), result per lane
-__device__ __forceinline__ double g8_fwd(const double (&Lr)[NQ], double r, int li) {
+template <bool ROW = false> __device__ __forceinline__ double g8_fwd(const double (&Lr)[NQ], double r, int li) {
   double y[NQ];
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
     double s = r;
 #pragma unroll
     for (int m = 0; m < k; ++m) s -= Lr[m] * y[m];
-    y[k] = g8_get(s * Lr[k], k);
+    y[k] = g8_get<ROW>(s * Lr[k], k);
   }
   double out = 0.0;
 #pragma unroll
@@ -130,22 +155,22 @@ __device__ __forceinline__ double g8_fwd(const double (&Lr)[NQ], double r, int l
 }
 
 // L L^T x = r (row layout)
-__device__ __forceinline__ double g8_solve(const double (&Lr)[NQ], double r, int li) {
+template <bool ROW = false> __device__ __forceinline__ double g8_solve(const double (&Lr)[NQ], double r, int li) {
   double y[NQ];
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
     double s = r;
 #pragma unroll
     for (int m = 0; m < k; ++m) s -= Lr[m] * y[m];
-    y[k] = g8_get(s * Lr[k], k);
+    y[k] = g8_get<ROW>(s * Lr[k], k);
   }
   double x[NQ];
 #pragma unroll
   for (int k = NQ - 1; k >= 0; --k) {
     double s = y[k];
 #pragma unroll
-    for (int m = k + 1; m < NQ; ++m) s -= g8_get(Lr[k], m) * x[m];
-    x[k] = s * g8_get(Lr[k], k);
+    for (int m = k + 1; m < NQ; ++m) s -= g8_get<ROW>(Lr[k], m) * x[m];
+    x[k] = s * g8_get<ROW>(Lr[k], k);
   }
   double out = 0.0;
 #pragma unroll

@@ -541,21 +541,16 @@ __device__ __forceinline__ double bcast(double v, int lane) {
 // lane k's value to every lane of its 16-lane row (DPP row_newbcast: one
 // v_mov_b64_dpp, no SGPR round trip).  The 7x7 algebra below lives on lanes
 // 0..6 of row 0; the other rows compute on their own (unused) lanes.
-template <int K> __device__ __forceinline__ double rowb_(double v) {
-  const long long x = __builtin_bit_cast(long long, v);
-  const long long r = __builtin_amdgcn_update_dpp(x, x, 0x150 + K, 0xf, 0xf, true);
-  return __builtin_bit_cast(double, r);
-}
 // k is a constant after unrolling: the switch folds away
 __device__ __forceinline__ double rowb(double v, int k) {
   switch (k) {
-    case 0: return rowb_<0>(v);
-    case 1: return rowb_<1>(v);
-    case 2: return rowb_<2>(v);
-    case 3: return rowb_<3>(v);
-    case 4: return rowb_<4>(v);
-    case 5: return rowb_<5>(v);
-    default: return rowb_<6>(v);
+    case 0: return g8_rowb<0>(v);
+    case 1: return g8_rowb<1>(v);
+    case 2: return g8_rowb<2>(v);
+    case 3: return g8_rowb<3>(v);
+    case 4: return g8_rowb<4>(v);
+    case 5: return g8_rowb<5>(v);
+    default: return g8_rowb<6>(v);
   }
 }
 

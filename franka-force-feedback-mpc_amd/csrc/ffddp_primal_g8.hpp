@@ -132,13 +132,13 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
     for (int k = 0; k < 3; ++k) apl[k] = aO[k] + c1[k] + c2[k];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      pee[k] = g8_get(o[k], 7);
-      vp[k] = g8_get(vpl[k], 7);
-      wee[k] = g8_get(w[k], 7);
-      ap0[k] = g8_get(apl[k], 7);
+      pee[k] = g8_get<true>(o[k], 7);
+      vp[k] = g8_get<true>(vpl[k], 7);
+      wee[k] = g8_get<true>(w[k], 7);
+      ap0[k] = g8_get<true>(apl[k], 7);
     }
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Ree[k] = g8_get(R[k], 7);
+    for (int k = 0; k < 9; ++k) Ree[k] = g8_get<true>(R[k], 7);
   }
   if (J) {
 #pragma unroll
@@ -260,8 +260,8 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
     double Lr[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-      const double sx = g8_get(Sv[0], k), sy = g8_get(Sv[1], k), sz = g8_get(Sv[2], k);
-      const double zx = g8_get(z[0], k), zy = g8_get(z[1], k), zz = g8_get(z[2], k);
+      const double sx = g8_get<true>(Sv[0], k), sy = g8_get<true>(Sv[1], k), sz = g8_get<true>(Sv[2], k);
+      const double zx = g8_get<true>(z[0], k), zy = g8_get<true>(z[1], k), zz = g8_get<true>(z[2], k);
       const double mkj = sx * Fl[0] + sy * Fl[1] + sz * Fl[2] + zx * Fa[0] + zy * Fa[1] + zz * Fa[2];
       Lr[k] = (k <= li) ? mkj : (li == k ? 1.0 : 0.0);
     }
@@ -269,13 +269,13 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
 #pragma unroll
       for (int k = 0; k < NQ; ++k) Lr[k] = (k == NQ - 1) ? 1.0 : 0.0;  // harmless identity row (not stored)
     }
-    g8_chol_rows(Lr, li);
+    g8_chol_rows<true>(Lr, li);
     if (J) {
 #pragma unroll
       for (int k = 0; k < NQ; ++k)
         if (k <= li) gp->L[tri(li, k)] = Lr[k];
     }
-    const double af = g8_solve(Lr, u - tau, li);
+    const double af = g8_solve<true>(Lr, u - tau, li);
     if (surface) {
       constexpr int c0 = NC == 1 ? 2 : 0;
       const double pstar[3] = {ref[0], ref[1], ref[2] - C.z_press};
@@ -287,7 +287,7 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
       for (int r = 0; r < NC; ++r) {
         Jc[r] = J ? jcol[c0 + r] : 0.0;
         gam[r] = ap0[c0 + r] + C.Kp * (pee[c0 + r] - pstar[c0 + r]) + C.Kd * vp[c0 + r];
-        Y[r] = g8_fwd(Lr, Jc[r], li);
+        Y[r] = g8_fwd<true>(Lr, Jc[r], li);
         if (J) {
           gp->Jc[r][li] = Jc[r];
           gp->Y[r][li] = Y[r];
@@ -309,7 +309,7 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
       double rhs = 0.0;
 #pragma unroll
       for (int r = 0; r < NC; ++r) rhs += Jc[r] * (-yl[r]);
-      a = af + g8_solve(Lr, rhs, li);
+      a = af + g8_solve<true>(Lr, rhs, li);
 #pragma unroll
       for (int r = 0; r < NC; ++r) lam[r] = -yl[r];
     } else {
