@@ -46,8 +46,8 @@ template <int CTRL> __device__ __forceinline__ int dpp32(int v) {
 #define G8_DPP 2
 #endif
 // Broadcast of group lane K.  Default (G8_DPP 2): row_newbcast of lane K and
-// of lane 8 + K (one v_mov_b64_dpp each: both 8-lane groups of the 16-lane
-// DPP row), each group keeping its own; 2-3 % faster line search than
+// of lane 8 + K under bank masks (one v_mov_b64_dpp each: both 8-lane groups
+// of the 16-lane DPP row get their own lane K); faster line search than
 // ds_swizzle BROADCAST(8, K) (G8_DPP 0), which goes through the LDS pipe.
 // G8_DPP 1: quad_perm [k,k,k,k] then row_shr:4 / row_shl:4 under a bank
 // mask (four 32-bit DPP moves; no faster than the swizzle).
@@ -58,10 +58,13 @@ template <int K> __device__ __forceinline__ double g8_rowb(double v) {
 }
 template <int K> __device__ __forceinline__ double g8_bc(double v) {
 #if G8_DPP == 2
-  // both groups of the 16-lane DPP row: row_newbcast of lane K and of lane
-  // 8 + K (one v_mov_b64_dpp each), then each group keeps its own
-  const double a = g8_rowb<K>(v), b = g8_rowb<8 + K>(v);
-  return (threadIdx.x & 8) ? b : a;
+  // both groups of the 16-lane DPP row: row_newbcast of lane 8 + K into
+  // banks 2-3 (lanes 8..15), then of lane K into banks 0-1 (lanes 0..7) of
+  // the same register: two v_mov_b64_dpp, no select
+  const long long x = __builtin_bit_cast(long long, v);
+  const long long t = __builtin_amdgcn_mov_dpp(x, 0x158 + K, 0xf, 0xC, false);
+  const long long r = __builtin_amdgcn_update_dpp(t, x, 0x150 + K, 0xf, 0x3, false);
+  return __builtin_bit_cast(double, r);
 #elif G8_DPP
   constexpr int qp = (K & 3) * 0x55;
   constexpr int sh = K < 4 ? 0x114 : 0x104;
