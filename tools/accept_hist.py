@@ -21,6 +21,7 @@ ee = R.R_MJ_FROM_PIN @ _abi.frame_placement(R.Q_NEUTRAL)[1]
 b = workload.make_batch(B, N, variant, _abi.gravity_torque, ee, seed=1234, fk=_abi.frame_placement)
 s = BatchedBoxFDDP(cfg, max_batch=B)
 prev_tr = np.zeros(B, np.int64)
+hist = np.zeros((10, B), np.int64)  # per-instance tried count per iteration (0: did not run)
 prev_fw = np.zeros(B, np.int64)
 for k in range(1, 11):
     s.solve(b, maxiter=k)
@@ -28,7 +29,10 @@ for k in range(1, 11):
     tr, fw = st[:, 1], st[:, 5]
     ran = fw > prev_fw  # instances that ran the forward pass of iteration k-1
     d = (tr - prev_tr)[ran]
+    hist[k - 1][ran] = d
     h = np.bincount(d, minlength=11)[1:11]
     print(f"iter {k - 1}: active {int(ran.sum()):5d}  tried-count hist (1..10) {h.tolist()}  "
           f"need>4: {int((d > 4).sum())}  need>1: {int((d > 1).sum())}")
     prev_tr, prev_fw = tr, fw
+if len(sys.argv) > 3:
+    np.save(sys.argv[3], hist)
