@@ -532,12 +532,6 @@ __device__ __forceinline__ void tri_rc(int e, int& r, int& c) {
 }
 
 // ---- 7x7 algebra with one row / variable per lane (lanes 0..6), uniform control flow ----
-__device__ __forceinline__ double bcast(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
-
 // lane k's value to every lane of its 16-lane row (DPP row_newbcast: one
 // v_mov_b64_dpp, no SGPR round trip).  The 7x7 algebra below lives on lanes
 // 0..6 of row 0; the other rows compute on their own (unused) lanes.
@@ -598,15 +592,16 @@ __device__ __forceinline__ double chol_solve_rows(const double (&Lr)[NU], double
   return out;
 }
 
-// sum / max over lanes 0..7 (lanes >= NU hold 0): DPP inside the first 8
-// lanes, the result read back from lane 0 (wave-uniform)
-__device__ __forceinline__ double sum8_u(double v) { return bcast(g8_sum(v), 0); }
-__device__ __forceinline__ double max8_u(double v) {
+// max over lanes 0..7 (lanes >= NU hold 0), in every lane of the group
+__device__ __forceinline__ double max8(double v) {
   v = fmax(v, dpp64<0x141>(v));  // row_half_mirror
   v = fmax(v, dpp64<0xB1>(v));   // quad_perm [1,0,3,2]
   v = fmax(v, dpp64<0x4E>(v));   // quad_perm [2,3,0,1]
-  return bcast(v, 0);
+  return v;
 }
+// a branch on lane 0's value of a condition (lane 0 holds the 8-lane sums /
+// maxima like every lane of its group): a ballot bit, no readlane round trip
+__device__ __forceinline__ bool lane0(bool c) { return (__ballot(c) & 1ull) != 0; }
 
 // crocoddyl::BoxQP::solve with variable i on lane i: projected Newton on the
 // free set, refactored when it changes, Armijo line search over the same
@@ -649,8 +644,8 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
       clmask = m;
     }
     const double dx = cl ? 0.0 : xsf - x;
-    if (max8_u(fabs(dx)) < C.qp_th_grad) break;
-    const double fold = sum8_u(0.5 * x * hx + q * x);
+    if (lane0(max8(fabs(dx)) < C.qp_th_grad)) break;
+    const double fold = g8_sum(0.5 * x * hx + q * x);
 #pragma unroll 1
     for (int ia = 0; ia < NTRIALS; ++ia) {
       const double al = C.alphas[ia];
@@ -658,9 +653,9 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
       double hxn = 0.0;
 #pragma unroll
       for (int j = 0; j < NU; ++j) hxn += hrow[j] * rowb(xn, j);
-      const double fnew = sum8_u(0.5 * xn * hxn + q * xn);
-      const double gd = sum8_u(g * (x - xn));
-      if (fold - fnew > C.qp_th_acceptstep * gd) {
+      const double fnew = g8_sum(0.5 * xn * hxn + q * xn);
+      const double gd = g8_sum(g * (x - xn));
+      if (lane0(fold - fnew > C.qp_th_acceptstep * gd)) {
         x = xn;
         break;
       }
