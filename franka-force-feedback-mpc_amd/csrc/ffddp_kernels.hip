@@ -665,7 +665,7 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
 }
 
 // LATE: the variant for the latency-bound iterations (few instances left):
-// phase C fully unrolled, 1 wave/SIMD register budget.  Both variants are
+// phase C fully unrolled (classical), 1 wave/SIMD register budget.  Both variants are
 // launched every iteration; the device-side active count picks the one that
 // works (late_max: the most active instances the LATE variant takes, so its
 // waves fit one per SIMD), the other one's blocks exit at once.
@@ -710,7 +710,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
   // this lane's lower-triangle entries of Q (phase C) and V (phase F), fixed for the whole pass
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 63) / 64;
-  constexpr int QC_N = LATE ? NQL : QC_UNROLL;  // phase C unroll
+  // phase C unroll: full in the classical latency variant; FF's 7 passes
+  // unrolled spill into AGPRs (1.5 % slower at B=1024), so not there
+  constexpr int QC_N = LATE ? (FF ? 1 : NQL) : QC_UNROLL;
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 63) / 64;
   int qrc[NQL], vij[NVL];
 #pragma unroll
