@@ -1735,6 +1735,11 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
         // the first pass as one wave per SIMD holds (8 groups per wave), so
         // the second pass (a whole extra rollout on the chain) is rarely needed
         if (h->fw_fill) n1 = std::max(n1, std::min(NTRIALS, 8 * h->n_simd / std::max(B, 1)));
+        // long horizons: a second pass is a rollout ~N node-calcs long, so
+        // once the first pass is 8 wide it takes all ten (N=100 point3d,
+        // B=1024: +4.5 %; at N=30 the two extra trials cost more than the
+        // rare second pass saves)
+        if (h->fw_fill && N >= 60 && n1 >= 8) n1 = NTRIALS;
         const bool late = it >= h->fw_late_it;
         auto fw = [&](int tr0, int ntr, int more) {
           const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
