@@ -167,7 +167,14 @@ def main():
     from ffddp.config import classical_preset, ff_preset
 
     rank, world, local_rank = shard.env_ranks()
-    shard.init("nccl", local_rank, world)
+    # FFDDP_BENCH_ONE_GPU=1: every rank on cuda:0 with gloo collectives, a
+    # one-GPU rehearsal of the N > 1 path (slices, max-over-ranks timing,
+    # gather); never how the metric is measured
+    if os.environ.get("FFDDP_BENCH_ONE_GPU") == "1":
+        shard.init("gloo", local_rank, world)
+        local_rank = 0
+    else:
+        shard.init("nccl", local_rank, world)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
