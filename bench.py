@@ -107,8 +107,9 @@ def pmc_traffic(variant, contact, B, N):
 
 def cpu_baseline(cfg, batch, maxiter: int, budget_s: float) -> dict:
     """The C++ scalar BoxFDDP (oracle/cpu) on the host cores: OpenMP over the
-    same instances, one per thread at a time; warm-up, then the median of 3
-    timed runs over the batch (bounded to about budget_s of CPU work)."""
+    same instances, one per thread at a time; warm-up, then the median of 5
+    timed runs over the sample (median of >= 5; the sample
+    is sized so the 5 runs take about budget_s of CPU time)."""
     from ffddp import _abi
     from oracle import cpu_fddp  # checker / baseline leg only
 
@@ -122,10 +123,11 @@ def cpu_baseline(cfg, batch, maxiter: int, budget_s: float) -> dict:
     t0 = time.perf_counter()
     cpu_fddp.solve_batch(rb, cs, warm, maxiter=maxiter, nthreads=threads)
     per_solve = (time.perf_counter() - t0) / warm.B * threads
-    n = int(min(batch.B, max(2 * threads, budget_s / 3.0 / max(per_solve, 1e-6) * threads)))
+    runs = 5
+    n = int(min(batch.B, max(2 * threads, budget_s / runs / max(per_solve, 1e-6) * threads)))
     sample = batch.slice(slice(0, n))
     times = []
-    for _ in range(3):
+    for _ in range(runs):
         t0 = time.perf_counter()
         out = cpu_fddp.solve_batch(rb, cs, sample, maxiter=maxiter, nthreads=threads)
         times.append(time.perf_counter() - t0)
@@ -134,7 +136,7 @@ def cpu_baseline(cfg, batch, maxiter: int, budget_s: float) -> dict:
         "value": n / med, "unit": "solves/s", "cores": threads, "kind": "port",
         "sample": f"first {n} of the {batch.B} instances of the same seeded workload; C++ scalar BoxFDDP "
                   f"(oracle/cpu/ffddp_cpu.cpp: the product's node models compiled for the host + a sequential "
-                  f"Crocoddyl-style solver), OpenMP {threads} threads, maxiter={maxiter}, median of 3 runs "
+                  f"Crocoddyl-style solver), OpenMP {threads} threads, maxiter={maxiter}, median of {runs} runs "
                   f"({med:.2f} s each; ok {float(np.mean(out['ok'])):.2f}, mean iter {float(np.mean(out['iter'])):.2f})",
     }
 
@@ -159,6 +161,8 @@ def main():
     ap.add_argument("--no-host-io", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the weak-scaling and random-regime extras")
     args = ap.parse_args()
+    if args.profile_only and args.no_profile:
+        ap.error("--profile-only runs only the profiling step: it cannot be combined with --no-profile")
 
     import torch
     import torch.distributed as dist
@@ -340,15 +344,25 @@ def main():
     host_io = None
     if not args.no_host_io and world == 1:
         # PCIe-inclusive rate of the host-array entry point (ffddp_solve_batch):
-        # H2D of the inputs + solve + D2H of xs/us/K/cost/...; reported beside
-        # `value`, never as `value`.
-        solver.solve(mine, maxiter=args.maxiter)
-        th0 = time.perf_counter()
-        reps = 3
-        for _ in range(reps):
-            solver.solve(mine, maxiter=args.maxiter)
-        th = (time.perf_counter() - th0) / reps
-        host_io = {"value": mine.B / th, "unit": "solves/s", "ms_per_step": th * 1e3}
+        # H2D of the inputs + solve + D2H of xs/us/K/cost/... per slice on the
+        # slice streams; reported beside `value`, never as `value` (DESIGN.md
+        # §7).  Pageable numpy arrays (through the library's page-locked
+        # staging), and page-locked output arrays (pinned_outputs: DMA
+        # straight into them).
+        host_io = {"unit": "solves/s"}
+        for key, hs in (("pageable", solver),
+                        ("pinned_outputs", BatchedBoxFDDP(cfg, max_batch=max(counts), device=local_rank,
+                                                          pinned_outputs=True))):
+            hs.solve(mine, maxiter=args.maxiter)
+            th0 = time.perf_counter()
+            reps = 5
+            for _ in range(reps):
+                hs.solve(mine, maxiter=args.maxiter)
+            th = (time.perf_counter() - th0) / reps
+            host_io[key] = {"value": mine.B / th, "ms_per_step": th * 1e3}
+            if hs is not solver:
+                hs.close()
+        host_io["value"] = host_io["pageable"]["value"]
 
     if rank == 0:
         base = None
@@ -364,7 +378,7 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": None,
+            "vs_baseline": None,  # BASELINE.md publishes no number for this metric
             "dtype": "f64",
             "data": f"synthetic (seeded workload.make_batch, {args.regime} regime"
                     + (": x0 near IK of the benchmark trajectory at t0~U(0,20)s" if args.regime == "tracking" else "")

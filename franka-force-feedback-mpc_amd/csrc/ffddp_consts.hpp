@@ -151,6 +151,7 @@ inline void fill_consts(const ffddp_robot& rb, const ffddp_ocp_config& c, DevCon
   k.reg_max = 1e9;
   k.reg_inc = 10.0;
   k.reg_dec = 10.0;
+  k.neg_rule = FFDDP_NEGSTEP_CROCODDYL;
   for (int i = 0; i < NTRIALS; ++i) k.alphas[i] = 1.0 / (double)(1 << i);
   k.qp_maxiter = 100;
   k.qp_th_acceptstep = 0.1;

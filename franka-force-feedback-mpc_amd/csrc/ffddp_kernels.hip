@@ -30,6 +30,7 @@
 #include <new>
 #include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ffddp_consts.hpp"
@@ -49,9 +50,6 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 #ifndef NODE_WAVES
 #define NODE_WAVES 2
 #endif
-#ifndef FW_WAVES
-#define FW_WAVES 2
-#endif
 #ifndef QC_UNROLL
 #define QC_UNROLL 1
 #endif
@@ -61,9 +59,9 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 
 struct InstState {
   double preg, cost, dg, dq, stop;
+  double ffeas;  // max |fs| of the last calcDiff (the trace's ||ffeas||)
   int is_feasible, was_feasible, done, ok, iter, recalc, accepted, bw_ok;
   int n_iters, n_trials, n_retries, n_backward, n_calc, n_forward;
-  int fw_more;  // (unused)
   int n_eval1, n_eval2;  // line-search trials evaluated by the first / second pass
 };
 
@@ -83,6 +81,8 @@ struct Dev {
   InstState* st;     // [B]
   int* alist;        // [2][B]  active-instance lists (slice-local indices), double-buffered over iterations
   int* acnt;         // [2]     their lengths
+  double* trace;     // [B][trace_it][FFDDP_TRACE_W] per-iteration records (CallbackVerbose), or null
+  int trace_it;
 };
 
 // Active-instance compaction.  Iteration it reads list (it & 1): the
@@ -111,7 +111,10 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
   const long nX = (long)d.B * (N + 1) * nx;
   const long nU = (long)d.B * N * NU;
   const long nK = (long)d.B * N * NU * nx;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nK; i += (long)gridDim.x * blockDim.x) {
+  const long nT = d.trace ? (long)d.B * d.trace_it * FFDDP_TRACE_W : 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nK || i < nT; i += (long)gridDim.x * blockDim.x) {
+    if (i < nT) d.trace[i] = __builtin_nan("");
+    if (i >= nK) continue;
     if (i < nX) d.xs[i] = xs_init[i];
     if (i < nU) {
       d.us[i] = us_init[i];
@@ -139,7 +142,7 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
       s.bw_ok = 0;
       s.n_iters = s.n_trials = s.n_retries = s.n_backward = s.n_calc = s.n_forward = 0;
       s.n_eval1 = s.n_eval2 = 0;
-      s.fw_more = 0;
+      s.ffeas = 0.0;
       d.st[i] = s;
     }
   }
@@ -434,6 +437,21 @@ __device__ __forceinline__ double wave_sum(double v) {
   return (r0 + r1) + (r2 + r3);
 }
 
+// max over the 64 lanes (values >= 0), wave-uniform result
+__device__ __forceinline__ double wave_max(double v) {
+  v = fmax(v, dpp64<0xB1>(v));
+  v = fmax(v, dpp64<0x4E>(v));
+  v = fmax(v, dpp64<0x141>(v));
+  v = fmax(v, dpp64<0x140>(v));
+  double m = v;
+#pragma unroll
+  for (int r = 16; r < 64; r += 16)
+    m = fmax(m, __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), r),
+                                 __builtin_amdgcn_readlane(__double2loint(v), r)));
+  return fmax(m, __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 0),
+                                  __builtin_amdgcn_readlane(__double2loint(v), 0)));
+}
+
 // ---------------------------------------------------------------------------
 // backward pass, one wavefront per instance (k_backward_w)
 //
@@ -451,7 +469,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 // instances hide each other's latency.  Gains (LLT / BoxQP on 7x7) stay on
 // lane 0.
 // ---------------------------------------------------------------------------
-constexpr int rec_words(int nx) { return ((147 + nx * nx + nx * 7 + 49 + nx + 7 + 1) + 3 + 7) & ~7; }
+constexpr int rec_words(int nx) { return ((147 + nx * nx + nx * 7 + 49 + nx + 7 + 1) + 3 + 15) & ~15; }
 
 __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -705,7 +723,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   double preg = st->preg;
   int retries = 0;
   bool fail_inst = false;
-  double dg = 0.0, dq = 0.0, stop = 0.0;
+  double dg = 0.0, dq = 0.0, stop = 0.0, ffl = 0.0;
   S.ulb[l] = C.u_lb[l < NU ? l : NU - 1];
   S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
   // this lane's lower-triangle entries of Q (phase C) and V (phase F), fixed for the whole pass
@@ -728,7 +746,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
     vij[k] = (i << 8) | j;
   }
   for (;;) {
-    dg = dq = stop = 0.0;
+    dg = dq = stop = ffl = 0.0;
     bool failed = false;
     // ---- terminal node: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N) ----
     {
@@ -761,6 +779,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         double vfs = 0.0;
         for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
         const double fj = S.fs[l];
+        ffl = fabs(fj);
         const double vx = rT[rec_off_Lx(NX) + l] + (feas ? 0.0 : vfs);
         if (!feas) {
           d.w[((long)b * (N + 1) + N) * NX + l] = vfs;
@@ -967,6 +986,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         for (int c = 0; c < NU; ++c) vx -= S.K[c * NX + l] * S.Qv[NX + c];
         if (!feas) vx += vfs;
         badv |= bad(fabs(vx)) ? 1 : 0;
+        ffl = fmax(ffl, fabs(S.fs[l]));
         if (!feas) {
           d.w[((long)b * (N + 1) + t) * NX + l] = vfs;
           cdg -= vx * S.fs[l];
@@ -1002,6 +1022,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       dg = wave_sum(dg);
       dq = wave_sum(dq);
       stop = wave_sum(stop);
+      ffl = wave_max(ffl);
       break;
     }
     retries++;
@@ -1016,6 +1037,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   if (l == 0) {
     st->preg = preg;
     st->n_retries += retries;
+    // the trial k_node read in place has been written into (xs, us): no
+    // later kernel may take it for the current iterate (k_commit)
+    st->accepted = -1;
     if (fail_inst) {
       st->bw_ok = 0;
       st->iter = iter;
@@ -1026,6 +1050,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       st->dg = dg;
       st->dq = dq;
       st->stop = stop;
+      st->ffeas = ffl;
       st->bw_ok = 1;
       st->n_backward += retries + 1;
       st->n_iters += 1;
@@ -1039,8 +1064,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 // joint-parallel (node_calc_g8), which shortens the dependent chain that
 // bounds this kernel.  Lane i < 7 carries joint i of x (q_i, v_i, FF tau_i).
 // ---------------------------------------------------------------------------
-// SolverFDDP::tryStep acceptance of trial tr for an instance in state s
-__device__ __forceinline__ bool trial_accepted(const DevConsts& C, const Dev& d, const InstState& s, int b, int tr) {
+// SolverFDDP::solve acceptance of trial tr (tryStep + expectedImprovement)
+// for an instance in state s; dV / dVexp / d1 of the trial out (trace)
+__device__ __forceinline__ bool trial_accepted(const DevConsts& C, const Dev& d, const InstState& s, int b, int tr,
+                                               double* o_dV = nullptr, double* o_dVexp = nullptr,
+                                               double* o_d1 = nullptr) {
   if (d.trial_fail[(long)b * NTRIALS + tr]) return false;
   const double a = C.alphas[tr];
   const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
@@ -1048,17 +1076,26 @@ __device__ __forceinline__ bool trial_accepted(const DevConsts& C, const Dev& d,
   const double dV = s.cost - cost_try;
   const double d0 = s.dg + dv, d1 = s.dq - 2.0 * dv;
   const double dVexp = a * (d0 + 0.5 * a * d1);
+  if (o_dV) {
+    *o_dV = dV;
+    *o_dVexp = dVexp;
+    *o_d1 = d1;
+  }
   if (dVexp >= 0) return fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp;
-  // ascent direction (closing gaps may raise the cost): only while infeasible,
-  // accepting a rise of up to th_acceptnegstep x the predicted one
-  return !s.is_feasible && dV > C.th_acceptnegstep * dVexp;
+  // ascent direction (closing the gaps may raise the cost): only while
+  // infeasible.  Crocoddyl's comparator is dV < th_acceptnegstep dVexp; the
+  // alternative accepts a rise of at most th_acceptnegstep x the predicted
+  // one (include/ffddp.h FFDDP_NEGSTEP_*)
+  if (s.is_feasible) return false;
+  return C.neg_rule == FFDDP_NEGSTEP_CROCODDYL ? dV < C.th_acceptnegstep * dVexp
+                                               : dV > C.th_acceptnegstep * dVexp;
 }
 
-// W: waves/SIMD occupancy target (2 while the batch is throughput-bound, 1 for
-// the latency-bound late iterations, where the register budget also holds the
-// next node's K row: PK = prefetch it one node ahead)
-template <int NC, bool FF, int W = FW_WAVES, bool PK = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_forward_g8(const DevConsts* __restrict__ Cg, Dev d,
+// one wave per SIMD: the register budget holds the next node's K row,
+// prefetched one node ahead (a 2-waves/SIMD variant without the prefetch
+// measured slower in every iteration)
+template <int NC, bool FF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_forward_g8(const DevConsts* __restrict__ Cg, Dev d,
                                                    const double* __restrict__ x0,
                                                    const double* __restrict__ node_ref,
                                                    const double* __restrict__ inst_ref,
@@ -1121,11 +1158,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_
       const long ub = (long)b * N + t;
       pus = J ? d.us[ub * NU + ji] : 0.0;
       pk = J ? d.k[ub * NU + ji] : 0.0;
-      if constexpr (PK) {
-        const double* K_t = d.K + ub * NU * nx + (long)ji * nx;
+      const double* K_t = d.K + ub * NU * nx + (long)ji * nx;
 #pragma unroll
-        for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
-      }
+      for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
     }
   };
   fetch(0);
@@ -1150,11 +1185,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_
       // u_i = us_i - alpha k_i - K_i (x - xs)
       double u = 0.0;
       {
-        if constexpr (!PK) {
-          const double* K_t = d.K + ((long)b * N + t) * NU * nx + (long)ji * nx;
-#pragma unroll
-          for (int m = 0; m < nx; ++m) pK[m] = J ? K_t[m] : 0.0;
-        }
         double acc = pus - pk * alpha;
         const double dq = xq_t - sq, dv = xv_t - sv, dtt = xt_t - stt;
 #pragma unroll
@@ -1244,10 +1274,17 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int 
   int acc = -1;
   double steplength = C.alphas[NTRIALS - 1];
   int tried = NTRIALS;
+  // dV, dVexp, d1 of the accepted (else the last finite) trial, for the trace
+  double tdV = __builtin_nan(""), tdVexp = __builtin_nan(""), td1 = __builtin_nan("");
   for (int tr = 0; tr < NTRIALS; ++tr) {
     const double a = C.alphas[tr];
     const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
-    if (trial_accepted(C, d, s, b, tr)) {
+    double e0 = tdV, e1 = tdVexp, e2 = td1;
+    const bool okt = trial_accepted(C, d, s, b, tr, &e0, &e1, &e2);
+    tdV = e0;
+    tdVexp = e1;
+    td1 = e2;
+    if (okt) {
       acc = tr;
       steplength = a;
       tried = tr + 1;
@@ -1274,6 +1311,21 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int 
       s.done = 1;
       s.ok = 0;
     }
+  }
+  // CallbackVerbose record of this iteration (before the stopping test, as
+  // the callbacks run in SolverFDDP::solve; none when preg reached reg_max)
+  if (d.trace && iter < d.trace_it && !s.done) {
+    double* r = d.trace + ((long)b * d.trace_it + iter) * FFDDP_TRACE_W;
+    r[0] = (double)iter;
+    r[1] = s.cost;
+    r[2] = s.stop;
+    r[3] = -td1;
+    r[4] = s.preg;
+    r[5] = s.preg;
+    r[6] = steplength;
+    r[7] = s.ffeas;
+    r[8] = tdV;
+    r[9] = tdVexp;
   }
   if (!s.done && s.was_feasible && s.stop < C.th_stop) {
     s.done = 1;
@@ -1515,6 +1567,27 @@ __global__ __launch_bounds__(64) void k_build(const ffddp_robot* __restrict__ rb
 // ===========================================================================
 // host side
 // ===========================================================================
+// copies of the host entry point, issued per slice by launch_solve_t: inputs
+// host -> device before the slice's first kernel, outputs device -> host
+// after its last; `done[k]` is recorded on slice k's stream after them
+struct HostIO {
+  struct In {
+    void* dev;
+    const void* host;
+    size_t per_inst;
+  } in[6];
+  struct Out {
+    void* host;
+    const void* dev;
+    size_t per_inst;
+  } out[5];
+  int n_in = 0, n_out = 0;
+  hipEvent_t* done = nullptr;
+  // filled by launch_solve_t: the slices [b0[k], b0[k] + bk[k])
+  int ns = 0;
+  int b0[8] = {0}, bk[8] = {0};
+};
+
 struct ffddp_handle {
   int device = 0;
   int max_batch = 0;
@@ -1529,6 +1602,15 @@ struct ffddp_handle {
   int32_t *out_iters = nullptr, *out_stats = nullptr;
   uint8_t* out_ok = nullptr;
   std::string err;
+  // host entry point: page-locked staging (inputs + outputs, max_batch),
+  // its stream and the per-slice completion events
+  char* stage = nullptr;
+  size_t stage_bytes = 0;
+  hipStream_t hstream = nullptr;
+  std::vector<hipEvent_t> hdone;
+  // per-iteration trace (ffddp_trace_enable)
+  double* trace = nullptr;
+  int trace_it = 0;
   // sub-batch streams: the batch is split into nstreams slices solved on their
   // own HIP streams, so latency-bound phases of one slice overlap with the
   // throughput-bound phases of another (FFDDP_STREAMS, default 4: three
@@ -1548,7 +1630,6 @@ struct ffddp_handle {
   // work and the second pass, needed there anyway, covers the rest; once most
   // instances are done the pass is latency-bound and 4 trials in one pass win
   std::vector<int> fw_sched{2, 2, 2, 2};
-  int fw_late_it = 0;  // first iteration using the 1-wave/SIMD line-search variant (FFDDP_FW_LATE_IT)
   int bw_late_max = -1;  // active instances up to which a slice's backward pass uses the latency variant
                          // (FFDDP_BW_LATE_MAX; -1: SIMDs / slices)
   int n_simd = 1024;     // SIMDs of the device (4 per CU)
@@ -1592,6 +1673,8 @@ void free_all(ffddp_handle* h) {
                 h->out_stats, h->out_ok};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  if (h->trace) (void)hipFree(h->trace);
+  if (h->stage) (void)hipHostFree(h->stage);
 }
 
 // event pair around a launch (only when profiling is enabled)
@@ -1641,6 +1724,7 @@ Dev dev_slice(const Dev& d0, int b0, int Bk, int k) {
   d.st += b0;
   d.alist += 2L * b0;
   d.acnt += 2 * k;
+  if (d.trace) d.trace += (long)b0 * d0.trace_it * FFDDP_TRACE_W;
   return d;
 }
 
@@ -1648,7 +1732,7 @@ template <int NC, bool FF>
 int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref, const double* iref,
                  const uint8_t* surf, const double* xs_init, const double* us_init, int maxiter, int is_feasible,
                  double* xs, double* us, double* K, double* cost, int32_t* iters, uint8_t* ok, double* fn_pred,
-                 int32_t* stats, hipStream_t s) {
+                 int32_t* stats, hipStream_t s, HostIO* io) {
   const int N = h->hc.N, nx = h->hc.nx;
   int S = h->nstreams;
   if (B < 64 * S) S = 1;
@@ -1690,6 +1774,21 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       if (sl[k].s != s) HIPCHK(h, hipStreamWaitEvent(sl[k].s, h->sev[0], 0));
   }
   const long nxl = nx, N1 = N + 1;
+  if (io) {
+    io->ns = S;
+    for (int k = 0; k < S; ++k) {
+      io->b0[k] = sl[k].b0;
+      io->bk[k] = sl[k].B;
+    }
+    // host entry point: each slice's inputs go up on its own stream, so slice
+    // k's copies overlap slice k-1's kernels
+    for (int k = 0; k < S; ++k)
+      for (int i = 0; i < io->n_in; ++i) {
+        const size_t o = (size_t)sl[k].b0 * io->in[i].per_inst;
+        HIPCHK(h, hipMemcpyAsync((char*)io->in[i].dev + o, (const char*)io->in[i].host + o,
+                                 (size_t)sl[k].B * io->in[i].per_inst, hipMemcpyHostToDevice, sl[k].s));
+      }
+  }
   for (int k = 0; k < S; ++k) {
     ProfScope p(h, sl[k].s, KC_INIT);
     const long b0 = sl[k].b0;
@@ -1740,15 +1839,10 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
         // B=1024: +4.5 %; at N=30 the two extra trials cost more than the
         // rare second pass saves)
         if (h->fw_fill && N >= 60 && n1 >= 8) n1 = NTRIALS;
-        const bool late = it >= h->fw_late_it;
         auto fw = [&](int tr0, int ntr, int more) {
           const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
-          if (late)
-            hipLaunchKernelGGL((k_forward_g8<NC, FF, 1, true>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
-                               surfk, tr0, ntr, more, it & 1);
-          else
-            hipLaunchKernelGGL((k_forward_g8<NC, FF>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk, tr0,
-                               ntr, more, it & 1);
+          hipLaunchKernelGGL((k_forward_g8<NC, FF>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk, tr0,
+                             ntr, more, it & 1);
         };
         {
           ProfScope p(h, ss, KC_FORWARD);
@@ -1783,9 +1877,19 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
                          x0 + b0 * nxl, nref + b0 * N1 * 6, iref + b0 * 21, surf + b0, cost + b0, iters + b0, ok + b0,
                          fn_pred ? fn_pred + 2 * b0 : nullptr, stats ? stats + b0 * FFDDP_NSTATS : nullptr);
     }
-    HIPCHK(h, hipMemcpyAsync(xs + b0 * N1 * nxl, d.xs, bxs * Bk, hipMemcpyDeviceToDevice, ss));
-    HIPCHK(h, hipMemcpyAsync(us + b0 * (long)N * NU, d.us, bus * Bk, hipMemcpyDeviceToDevice, ss));
-    HIPCHK(h, hipMemcpyAsync(K + b0 * (long)N * NU * nx, d.K, bks * Bk, hipMemcpyDeviceToDevice, ss));
+    // device outputs (dev entry point), or page-locked host memory (host
+    // entry point: the slice's results go down as soon as it finishes)
+    HIPCHK(h, hipMemcpyAsync(xs + b0 * N1 * nxl, d.xs, bxs * Bk, hipMemcpyDefault, ss));
+    HIPCHK(h, hipMemcpyAsync(us + b0 * (long)N * NU, d.us, bus * Bk, hipMemcpyDefault, ss));
+    HIPCHK(h, hipMemcpyAsync(K + b0 * (long)N * NU * nx, d.K, bks * Bk, hipMemcpyDefault, ss));
+    if (io) {
+      for (int i = 0; i < io->n_out; ++i) {
+        const size_t o = (size_t)b0 * io->out[i].per_inst;
+        HIPCHK(h, hipMemcpyAsync((char*)io->out[i].host + o, (const char*)io->out[i].dev + o,
+                                 (size_t)Bk * io->out[i].per_inst, hipMemcpyDeviceToHost, ss));
+      }
+      HIPCHK(h, hipEventRecord(io->done[k], ss));
+    }
   }
   if (hipGetLastError() != hipSuccess) return fail(h, FFDDP_E_DEVICE, "kernel launch failed");
   if (S > 1) {
@@ -1801,11 +1905,11 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
 int launch_solve(ffddp_handle* h, int B, const double* x0, const double* nref, const double* iref,
                  const uint8_t* surf, const double* xs_init, const double* us_init, int maxiter, int is_feasible,
                  double* xs, double* us, double* K, double* cost, int32_t* iters, uint8_t* ok, double* fn_pred,
-                 int32_t* stats, hipStream_t s) {
+                 int32_t* stats, hipStream_t s, HostIO* io = nullptr) {
   const bool ff = h->hc.variant == FFDDP_FORCE_FEEDBACK;
   const int nc = h->hc.nc;
 #define FFDDP_LS(NC_, FF_) \
-  launch_solve_t<NC_, FF_>(h, B, x0, nref, iref, surf, xs_init, us_init, maxiter, is_feasible, xs, us, K, cost, iters, ok, fn_pred, stats, s)
+  launch_solve_t<NC_, FF_>(h, B, x0, nref, iref, surf, xs_init, us_init, maxiter, is_feasible, xs, us, K, cost, iters, ok, fn_pred, stats, s, io)
   if (nc == 1) return ff ? FFDDP_LS(1, true) : FFDDP_LS(1, false);
   return ff ? FFDDP_LS(3, true) : FFDDP_LS(3, false);
 #undef FFDDP_LS
@@ -1816,6 +1920,38 @@ void launch_node(ffddp_handle* h, Dev d, int B, hipStream_t s, int force_all) {
   const long nodes = (long)B * (h->hc.N + 1);
   hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, s, h->dc,
                      d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all, 0);
+}
+
+// page-locked (hipHostMalloc'd / registered) host memory?
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// host memcpy, split over a few threads for large copies (a single core
+// moves ~10 GB/s; the staging copies of a B = 4096 solve are ~150 MB)
+void host_copy(void* dst, const void* src, size_t n) {
+  constexpr size_t kChunk = size_t(4) << 20;
+  const size_t nt = std::min<size_t>(8, n / kChunk);
+  if (nt <= 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  const size_t part = (n + nt - 1) / nt;
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (size_t i = 1; i < nt; ++i) {
+    const size_t o = i * part;
+    if (o >= n) break;
+    const size_t len = std::min(part, n - o);
+    th.emplace_back([=] { std::memcpy((char*)dst + o, (const char*)src + o, len); });
+  }
+  std::memcpy(dst, src, std::min(part, n));
+  for (std::thread& t : th) t.join();
 }
 
 bool valid_cfg(const ffddp_ocp_config& c) {
@@ -1859,7 +1995,6 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
       const int v = std::atoi(ns);
       h->nstreams = v < 1 ? 1 : (v > 8 ? 8 : v);
     }
-    if (const char* fl = std::getenv("FFDDP_FW_LATE_IT")) h->fw_late_it = std::atoi(fl);
     if (const char* bl = std::getenv("FFDDP_BW_LATE_MAX")) h->bw_late_max = std::atoi(bl);
     if (const char* ff = std::getenv("FFDDP_FW_FILL")) h->fw_fill = std::atoi(ff) != 0;
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
@@ -1974,6 +2109,8 @@ void ffddp_destroy(ffddp_handle* h) {
   for (hipEvent_t e : h->sev) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->stg) (void)hipEventDestroy(e);
   for (hipStream_t st : h->streams) (void)hipStreamDestroy(st);
+  for (hipEvent_t e : h->hdone) (void)hipEventDestroy(e);
+  if (h->hstream) (void)hipStreamDestroy(h->hstream);
   free_all(h);
   delete h;
 }
@@ -2006,27 +2143,163 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
   if (!x0 || !node_ref || !inst_ref || !surface || !xs_init || !us_init || !xs || !us || !K || !cost || !iters || !ok)
     return fail(h, FFDDP_E_INVALID, "null pointer");
   HIPCHK(h, hipSetDevice(h->device));
-  const long N = h->hc.N, nx = h->hc.nx;
-  const size_t bx = (size_t)B * (N + 1) * nx * 8, bu = (size_t)B * N * NU * 8, bk = (size_t)B * N * NU * nx * 8;
-  HIPCHK(h, hipMemcpy(h->in_x0, x0, (size_t)B * nx * 8, hipMemcpyHostToDevice));
-  HIPCHK(h, hipMemcpy(h->in_nref, node_ref, (size_t)B * (N + 1) * 6 * 8, hipMemcpyHostToDevice));
-  HIPCHK(h, hipMemcpy(h->in_iref, inst_ref, (size_t)B * 21 * 8, hipMemcpyHostToDevice));
-  HIPCHK(h, hipMemcpy(h->in_surf, surface, (size_t)B, hipMemcpyHostToDevice));
-  HIPCHK(h, hipMemcpy(h->in_xs, xs_init, bx, hipMemcpyHostToDevice));
-  HIPCHK(h, hipMemcpy(h->in_us, us_init, bu, hipMemcpyHostToDevice));
+  const size_t N = (size_t)h->hc.N, nx = (size_t)h->hc.nx;
+  // per-instance bytes: inputs x0, node_ref, inst_ref, surface, xs_init, us_init;
+  // outputs xs, us, K, cost, iters, ok, fn_pred, stats
+  const size_t per[14] = {nx * 8, (N + 1) * 6 * 8, 21 * 8, 1, (N + 1) * nx * 8, N * NU * 8,
+                          (N + 1) * nx * 8, N * NU * 8, N * NU * nx * 8, 8, 4, 1, 16, FFDDP_NSTATS * 4};
+  size_t off[14], tot = 0;
+  for (int i = 0; i < 14; ++i) {
+    off[i] = tot;
+    tot += ((per[i] * (size_t)h->max_batch + 255) / 256) * 256;
+  }
+  if (!h->stage) {
+    if (hipHostMalloc((void**)&h->stage, tot, hipHostMallocDefault) != hipSuccess) {
+      h->stage = nullptr;
+      (void)hipGetLastError();
+      return fail(h, FFDDP_E_OOM, "hipHostMalloc (staging) failed");
+    }
+    h->stage_bytes = tot;
+  }
+  if (!h->hstream) HIPCHK(h, hipStreamCreateWithFlags(&h->hstream, hipStreamNonBlocking));
+  while (h->hdone.size() < 8) {
+    hipEvent_t e;
+    HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    h->hdone.push_back(e);
+  }
+  HostIO io;
+  io.done = h->hdone.data();
+  // inputs: page-locked caller memory goes up directly, pageable memory
+  // through the staging buffer (one parallel host copy before the launches)
+  const void* uin[6] = {x0, node_ref, inst_ref, surface, xs_init, us_init};
+  void* din[6] = {h->in_x0, h->in_nref, h->in_iref, h->in_surf, h->in_xs, h->in_us};
+  for (int i = 0; i < 6; ++i) {
+    const void* src = uin[i];
+    if (!host_pinned(src)) {
+      host_copy(h->stage + off[i], src, per[i] * (size_t)B);
+      src = h->stage + off[i];
+    }
+    io.in[io.n_in++] = HostIO::In{din[i], src, per[i]};
+  }
+  // outputs: slice by slice into page-locked caller memory, else into the
+  // staging buffer and from there into the caller's arrays as each slice ends
+  void* uout[8] = {xs, us, K, cost, iters, ok, fn_pred, stats};
+  void* hout[8];
+  bool staged[8];
+  for (int i = 0; i < 8; ++i) {
+    staged[i] = uout[i] != nullptr && !host_pinned(uout[i]);
+    hout[i] = uout[i] == nullptr ? nullptr : (staged[i] ? (void*)(h->stage + off[6 + i]) : uout[i]);
+  }
+  const void* dsmall[5] = {h->out_cost, h->out_iters, h->out_ok, h->out_fn, h->out_stats};
+  for (int i = 0; i < 5; ++i)
+    if (hout[3 + i]) io.out[io.n_out++] = HostIO::Out{hout[3 + i], dsmall[i], per[9 + i]};
   int rc = launch_solve(h, B, h->in_x0, h->in_nref, h->in_iref, h->in_surf, h->in_xs, h->in_us, maxiter, is_feasible,
-                        h->out_xs, h->out_us, h->out_K, h->out_cost, h->out_iters, h->out_ok, h->out_fn,
-                        h->out_stats, nullptr);
-  if (rc) return rc;
-  HIPCHK(h, hipDeviceSynchronize());
-  HIPCHK(h, hipMemcpy(xs, h->out_xs, bx, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy(us, h->out_us, bu, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy(K, h->out_K, bk, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy(cost, h->out_cost, (size_t)B * 8, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy(iters, h->out_iters, (size_t)B * 4, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy(ok, h->out_ok, (size_t)B, hipMemcpyDeviceToHost));
-  if (fn_pred) HIPCHK(h, hipMemcpy(fn_pred, h->out_fn, (size_t)B * 2 * 8, hipMemcpyDeviceToHost));
-  if (stats) HIPCHK(h, hipMemcpy(stats, h->out_stats, (size_t)B * FFDDP_NSTATS * 4, hipMemcpyDeviceToHost));
+                        (double*)hout[0], (double*)hout[1], (double*)hout[2], h->out_cost, h->out_iters, h->out_ok,
+                        h->out_fn, h->out_stats, h->hstream, &io);
+  if (rc) {
+    (void)hipStreamSynchronize(h->hstream);
+    return rc;
+  }
+  for (int k = 0; k < io.ns; ++k) {
+    HIPCHK(h, hipEventSynchronize(io.done[k]));
+    for (int i = 0; i < 8; ++i) {
+      if (!staged[i]) continue;
+      const size_t o = (size_t)io.b0[k] * per[6 + i];
+      host_copy((char*)uout[i] + o, (const char*)hout[i] + o, (size_t)io.bk[k] * per[6 + i]);
+    }
+  }
+  HIPCHK(h, hipStreamSynchronize(h->hstream));
+  return 0;
+}
+
+int ffddp_host_alloc(size_t bytes, void** p) {
+  if (!p) return FFDDP_E_INVALID;
+  *p = nullptr;
+  if (hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    *p = nullptr;
+    (void)hipGetLastError();
+    return FFDDP_E_OOM;
+  }
+  return 0;
+}
+
+int ffddp_host_free(void* p) {
+  if (!p) return 0;
+  return hipHostFree(p) == hipSuccess ? 0 : FFDDP_E_DEVICE;
+}
+
+int ffddp_get_solver_params(const ffddp_handle* h, ffddp_solver_params* p) {
+  if (!h || !p) return FFDDP_E_INVALID;
+  const DevConsts& c = h->hc;
+  *p = ffddp_solver_params{};
+  p->th_stop = c.th_stop;
+  p->th_grad = c.th_grad;
+  p->th_acceptstep = c.th_acceptstep;
+  p->th_acceptnegstep = c.th_acceptnegstep;
+  p->th_stepdec = c.th_stepdec;
+  p->th_stepinc = c.th_stepinc;
+  p->reg_min = c.reg_min;
+  p->reg_max = c.reg_max;
+  p->reg_incfactor = c.reg_inc;
+  p->reg_decfactor = c.reg_dec;
+  p->neg_step_rule = c.neg_rule;
+  return 0;
+}
+
+int ffddp_set_solver_params(ffddp_handle* h, const ffddp_solver_params* p) {
+  if (!h || !p) return FFDDP_E_INVALID;
+  const double v[10] = {p->th_stop, p->th_grad, p->th_acceptstep, p->th_acceptnegstep, p->th_stepdec,
+                        p->th_stepinc, p->reg_min, p->reg_max, p->reg_incfactor, p->reg_decfactor};
+  for (double x : v)
+    if (!std::isfinite(x) || x < 0.0) return fail(h, FFDDP_E_INVALID, "solver parameters must be finite and >= 0");
+  if (!(p->reg_min > 0.0) || p->reg_max < p->reg_min || !(p->reg_incfactor > 1.0) || !(p->reg_decfactor > 1.0))
+    return fail(h, FFDDP_E_INVALID, "need 0 < reg_min <= reg_max and reg factors > 1");
+  if (p->neg_step_rule != FFDDP_NEGSTEP_CROCODDYL && p->neg_step_rule != FFDDP_NEGSTEP_BOUNDED_RISE)
+    return fail(h, FFDDP_E_INVALID, "neg_step_rule must be FFDDP_NEGSTEP_CROCODDYL or FFDDP_NEGSTEP_BOUNDED_RISE");
+  DevConsts c = h->hc;
+  c.th_stop = p->th_stop;
+  c.th_grad = p->th_grad;
+  c.th_acceptstep = p->th_acceptstep;
+  c.th_acceptnegstep = p->th_acceptnegstep;
+  c.th_stepdec = p->th_stepdec;
+  c.th_stepinc = p->th_stepinc;
+  c.reg_min = p->reg_min;
+  c.reg_max = p->reg_max;
+  c.reg_inc = p->reg_incfactor;
+  c.reg_dec = p->reg_decfactor;
+  c.neg_rule = p->neg_step_rule;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipDeviceSynchronize());  // no solve in flight reads the constants while they change
+  HIPCHK(h, hipMemcpy(h->dc, &c, sizeof(DevConsts), hipMemcpyHostToDevice));
+  h->hc = c;
+  return 0;
+}
+
+int ffddp_trace_enable(ffddp_handle* h, int max_iters) {
+  if (!h || max_iters < 0) return FFDDP_E_INVALID;
+  HIPCHK(h, hipSetDevice(h->device));
+  if (h->trace) {
+    HIPCHK(h, hipDeviceSynchronize());
+    (void)hipFree(h->trace);
+  }
+  h->trace = nullptr;
+  h->trace_it = 0;
+  h->d.trace = nullptr;
+  h->d.trace_it = 0;
+  if (max_iters == 0) return 0;
+  if (int rc = dalloc(h, &h->trace, (size_t)h->max_batch * max_iters * FFDDP_TRACE_W)) return rc;
+  h->trace_it = max_iters;
+  h->d.trace = h->trace;
+  h->d.trace_it = max_iters;
+  return 0;
+}
+
+int ffddp_trace_read(ffddp_handle* h, int B, double* out) {
+  if (!h || !out || B < 0 || B > h->max_batch) return FFDDP_E_INVALID;
+  if (!h->trace) return fail(h, FFDDP_E_INVALID, "trace not enabled (ffddp_trace_enable)");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipDeviceSynchronize());  // diagnostic read: every stream's solve has finished
+  HIPCHK(h, hipMemcpy(out, h->trace, (size_t)B * h->trace_it * FFDDP_TRACE_W * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -52,6 +52,7 @@ struct DevConsts {
   // solver constants (crocoddyl SolverBoxFDDP / BoxQP)
   double th_stop, th_grad, th_acceptstep, th_acceptnegstep, th_stepdec, th_stepinc;
   double reg_min, reg_max, reg_inc, reg_dec;
+  int neg_rule;  // FFDDP_NEGSTEP_* : ascent-direction acceptance comparator
   double alphas[NTRIALS];
   int qp_maxiter;
   double qp_th_acceptstep, qp_th_grad, qp_reg;
@@ -66,7 +67,9 @@ FFD_HD int rec_off_Lx(int nx) { return rec_off_Luu(nx) + 49; }
 FFD_HD int rec_off_Lu(int nx) { return rec_off_Lx(nx) + nx; }
 FFD_HD int rec_off_cost(int nx) { return rec_off_Lu(nx) + 7; }
 FFD_HD int rec_off_lam(int nx) { return rec_off_cost(nx) + 1; }
-FFD_HD int rec_size(int nx) { return (rec_off_lam(nx) + 3 + 7) & ~7; }
+// padded to a multiple of 16 words (128 B): every node record starts on a
+// cache-line boundary, so k_node's record writes cover whole lines
+FFD_HD int rec_size(int nx) { return (rec_off_lam(nx) + 3 + 15) & ~15; }
 
 // ---------------------------------------------------------------------------
 // log3 / Jlog3 (pinocchio)

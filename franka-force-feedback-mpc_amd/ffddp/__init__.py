@@ -6,3 +6,4 @@ Host Python -> ctypes -> C-ABI (include/ffddp.h) -> hand-written HIP kernels.
 """
 from .config import OcpConfig, classical_preset, ff_preset  # noqa: F401
 from .solver import BatchedBoxFDDP, FfddpError  # noqa: F401
+from .callbacks import CallbackVerbose  # noqa: F401

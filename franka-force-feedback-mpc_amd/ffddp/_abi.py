@@ -36,9 +36,19 @@ SYMBOLS = (
     "ffddp_plant_destroy",
     "ffddp_plant_step",
     "ffddp_plant_step_dev",
+    "ffddp_get_solver_params",
+    "ffddp_set_solver_params",
+    "ffddp_trace_enable",
+    "ffddp_trace_read",
+    "ffddp_host_alloc",
+    "ffddp_host_free",
 )
 PLANT_OBS = 69
 NSTATS = 8
+TRACE_W = 10
+TRACE_FIELDS = ("iter", "cost", "stop", "grad", "preg", "dreg", "step", "ffeas", "dV", "dV_exp")
+NEGSTEP_CROCODDYL = 0
+NEGSTEP_BOUNDED_RISE = 1
 KERNEL_CLASSES = ("init", "node", "backward", "forward", "accept", "commit", "finalize", "forward2", "primal")
 
 
@@ -100,6 +110,38 @@ class OcpConfig(C.Structure):
         ("w_friction_cone", C.c_double),
         ("mu", C.c_double),
     ]
+
+
+class SolverParams(C.Structure):
+    """ffddp_solver_params: crocoddyl.SolverBoxFDDP / SolverFDDP properties."""
+
+    _fields_ = [
+        ("th_stop", C.c_double),
+        ("th_grad", C.c_double),
+        ("th_acceptstep", C.c_double),
+        ("th_acceptnegstep", C.c_double),
+        ("th_stepdec", C.c_double),
+        ("th_stepinc", C.c_double),
+        ("reg_min", C.c_double),
+        ("reg_max", C.c_double),
+        ("reg_incfactor", C.c_double),
+        ("reg_decfactor", C.c_double),
+        ("neg_step_rule", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+def solver_params(use_box: bool = True, **overrides) -> SolverParams:
+    """SolverParams with the SolverBoxFDDP (use_box) / SolverFDDP defaults the
+    library's handles start from (ffddp_consts.hpp fill_consts), then `overrides`."""
+    p = SolverParams()
+    vals = dict(th_stop=5e-5 if use_box else 1e-9, th_grad=1e-12, th_acceptstep=0.1, th_acceptnegstep=2.0,
+                th_stepdec=0.5, th_stepinc=0.01, reg_min=1e-9, reg_max=1e9, reg_incfactor=10.0, reg_decfactor=10.0,
+                neg_step_rule=NEGSTEP_CROCODDYL)
+    vals.update(overrides)
+    for k, v in vals.items():
+        setattr(p, k, v)
+    return p
 
 
 class Task(C.Structure):
@@ -260,6 +302,18 @@ def load() -> C.CDLL:
     lib.ffddp_plant_step.restype = C.c_int
     lib.ffddp_plant_step_dev.argtypes = [C.c_void_p, C.c_int] + [vp] * 4 + [C.c_int, vp, vp, vp]
     lib.ffddp_plant_step_dev.restype = C.c_int
+    lib.ffddp_get_solver_params.argtypes = [C.c_void_p, C.POINTER(SolverParams)]
+    lib.ffddp_get_solver_params.restype = C.c_int
+    lib.ffddp_set_solver_params.argtypes = [C.c_void_p, C.POINTER(SolverParams)]
+    lib.ffddp_set_solver_params.restype = C.c_int
+    lib.ffddp_trace_enable.argtypes = [C.c_void_p, C.c_int]
+    lib.ffddp_trace_enable.restype = C.c_int
+    lib.ffddp_trace_read.argtypes = [C.c_void_p, C.c_int, dp]
+    lib.ffddp_trace_read.restype = C.c_int
+    lib.ffddp_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
+    lib.ffddp_host_alloc.restype = C.c_int
+    lib.ffddp_host_free.argtypes = [C.c_void_p]
+    lib.ffddp_host_free.restype = C.c_int
     _lib = lib
     return lib
 
@@ -272,6 +326,42 @@ def dptr(a: np.ndarray):
 def iptr(a: np.ndarray):
     assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
     return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+class _PinnedBlock:
+    """One ffddp_host_alloc allocation; freed when the last array viewing it
+    is gone (every array's buffer keeps the block alive)."""
+
+    def __init__(self, nbytes: int):
+        self._lib = load()
+        p = C.c_void_p()
+        rc = self._lib.ffddp_host_alloc(max(int(nbytes), 1), C.byref(p))
+        if rc != 0:
+            raise MemoryError(f"ffddp_host_alloc({nbytes}) failed ({rc})")
+        self.ptr = p
+        self.buf = (C.c_char * max(int(nbytes), 1)).from_address(p.value)
+        self.buf._owner = self
+
+    def __del__(self):
+        try:
+            if self.ptr is not None and self.ptr.value:
+                self._lib.ffddp_host_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
+def pinned_arrays(specs) -> dict:
+    """numpy arrays in one page-locked host allocation (ffddp_host_alloc):
+    ffddp_solve_batch copies such arrays by DMA on the slice streams instead
+    of through its staging buffer.  specs: {name: (shape, dtype)}."""
+    offs, tot = {}, 0
+    for k, (shape, dt) in specs.items():
+        offs[k] = tot
+        tot += (int(np.prod(shape)) * np.dtype(dt).itemsize + 255) // 256 * 256
+    blk = _PinnedBlock(tot)
+    return {k: np.frombuffer(blk.buf, dtype=dt, count=int(np.prod(shape)), offset=offs[k]).reshape(shape)
+            for k, (shape, dt) in specs.items()}
 
 
 def uptr(a: np.ndarray):

@@ -23,6 +23,7 @@ import numpy as np
 
 from . import _abi
 from . import robot as R
+from .callbacks import CallbackVerbose
 from .config import OcpConfig
 from .solver import BatchedBoxFDDP
 from .workload import Batch
@@ -222,6 +223,8 @@ class _MPCBase:
                           "surface_mode": False, "unstable": False, "fn_pred": np.nan}
         self.ocp = self._ocp_config()
         self._solver = BatchedBoxFDDP(self.ocp, max_batch=1, device=device)
+        if self.cfg.verbose:  # crocoddyl_classical.py:352-353, 360-361
+            self._solver.setCallbacks([CallbackVerbose()], max_iters=max(int(self.cfg.max_iters), 1))
 
     # -- frames (crocoddyl_classical.py:199-258) -------------------------------------
     @property
@@ -450,6 +453,15 @@ class ClassicalCrocoddylMPC(_MPCBase):
             "unstable": bool(unstable), "fn_pred": float(fn_pred) if np.isfinite(fn_pred) else np.nan,
             "solved_now": bool(solved_now), "policy_idx": int(policy_idx),
         }
+        if (self._k % self.cfg.debug_every) == 0:  # crocoddyl_classical.py:420-428
+            fn = float(getattr(obs, "f_contact_normal", 0.0))
+            ee_z = float(obs.ee_pos[2]) if getattr(obs, "ee_pos", None) is not None else np.nan
+            print(
+                f"[MPC] t={t:6.3f} ok={ok} cost={cost:.2e} iters={iters:2d} "
+                f"|tau_raw|∞={np.max(np.abs(tau_raw)):.2f} |tau_cmd|∞={np.max(np.abs(tau_cmd)):.2f} "
+                f"surf={int(surface_now)} fn={fn:.2f} fn_pred={fn_pred:.2f} ee_z={ee_z:.4f} "
+                f"solve={int(solved_now)} i={int(policy_idx)} unstable={int(unstable)}"
+            )
         if not solved_now:
             self._rollout_shift()
         return tau_cmd
@@ -671,6 +683,17 @@ class ForceFeedbackCrocoddylMPC(_MPCBase):
             "unstable": bool(unstable), "fn_pred": fin(fn_pred), "fn_pred_raw": fin(fn_pred_raw),
             "fn_pred_corr": fin(self._fn_pred_corr), "solved_now": bool(solved_now), "policy_idx": int(policy_idx),
         }
+        if (self._k % self.cfg.debug_every) == 0:  # crocoddyl_force_feedback.py:673-683
+            fn = float(getattr(obs, "f_contact_normal", 0.0))
+            ee_z = float(obs.ee_pos[2]) if getattr(obs, "ee_pos", None) is not None else np.nan
+            print(
+                f"[MPC] t={t:6.3f} ok={ok} cost={cost:.2e} iters={iters:2d} "
+                f"|tau_des|∞={np.max(np.abs(tau_des)):.2f} "
+                f"|tau_raw|∞={np.max(np.abs(tau_raw)):.2f} |tau_cmd|∞={np.max(np.abs(tau_cmd)):.2f} "
+                f"|tau_state|∞={np.max(np.abs(tau_hat)):.2f} "
+                f"surf={int(surface_now)} fn={fn:.2f} fn_pred={fn_pred:.2f} corr={self._fn_pred_corr:.2f} "
+                f"ee_z={ee_z:.4f} solve={int(solved_now)} i={int(policy_idx)} unstable={int(unstable)}"
+            )
         if not solved_now:
             self._rollout_shift()
         return tau_cmd

@@ -217,9 +217,13 @@ def _sweep_instances(scenarios: Sequence[str], seeds: int):
 
 def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilted_15", "actuation_uncertainty"),
               seeds: int = 256, total_time: float = 4.0, rank: int = 0, world: int = 1, device: int = 0,
-              q_sigma: float = 0.02, verbose: bool = True) -> dict:
+              q_sigma: float = 0.02, verbose: bool = True, record: Sequence[int] = ()) -> dict:
     """Closed-loop sweep of len(scenarios) * seeds instances; this rank runs
-    its contiguous shard.  Returns per-instance summary arrays (this shard)."""
+    its contiguous shard.  Returns per-instance summary arrays (this shard).
+    record: shard-local instance indices whose controller inputs (the plant
+    record as the controller sees it, after any measurement noise) and
+    commanded torques are kept per tick, with what a scalar controller needs
+    to replay them (the task, the config, the start states)."""
     names, tilt, scale, seed = _sweep_instances(scenarios, seeds)
     n_all = len(names)
     per = (n_all + world - 1) // world
@@ -263,6 +267,10 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
             inj[b] = ScenarioUncertaintyInjector(dt=plant.dt, nu=7, config=uc)
     steps = int(total_time / plant.dt)
     series = {k: np.zeros((steps, B)) for k in ("t", "err_tan", "err_3d", "fn_meas", "contact")}
+    rec_idx = [int(i) for i in record]
+    rec_obs = np.zeros((steps, len(rec_idx), plant.obs.shape[1]))
+    rec_tau = np.zeros((steps, len(rec_idx), 7))
+    rec_t = np.zeros(steps)
     obs = plant.obs.copy()
     t = 0.0
     wall0 = time.perf_counter()
@@ -278,6 +286,11 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
         tc = time.perf_counter()
         tau = mpc.compute_control(q, v, bias, fn, ee[:, 2], t)
         ctrl_s += time.perf_counter() - tc
+        if rec_idx:
+            rec_t[k] = t
+            rec_obs[k] = obs[rec_idx]
+            rec_obs[k][:, 0:7], rec_obs[k][:, 7:14] = q[rec_idx], v[rec_idx]
+            rec_tau[k] = tau[rec_idx]
         tau_app = tau * scale
         for b, j in inj.items():
             tau_app[b] = j.command_for_plant(tau[b])
@@ -305,8 +318,12 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
                             series["fn_meas"][:, b], series["contact"][:, b], float(cfg.fn_des), t_cp)
         for k_ in keys:
             per_inst[k_][b] = s[k_]
-    return dict(names=names, seed=seed, per_instance=per_inst, ticks=steps, wall_s=wall, controller_s=ctrl_s,
-                instances=B, shard=(lo, hi), n_all=n_all)
+    out = dict(names=names, seed=seed, per_instance=per_inst, ticks=steps, wall_s=wall, controller_s=ctrl_s,
+               instances=B, shard=(lo, hi), n_all=n_all)
+    if rec_idx:
+        out["record"] = dict(index=np.array(rec_idx), t=rec_t, obs=rec_obs, tau=rec_tau, q0=q0[rec_idx], traj=traj,
+                             config=cfg, dt=plant.dt)
+    return out
 
 
 SUMMARY_KEYS = ("rms_tangential_error", "rms_tangential_error_contact_phase", "rms_3d_error", "avg_abs_force_err",

@@ -9,6 +9,10 @@ Mirrors what the reference uses of crocoddyl.SolverBoxFDDP
 
 with a leading batch axis.  Numerical failure never raises (ok[b] = False,
 like Crocoddyl); API / device errors raise RuntimeError.
+
+Solver properties (th_stop, th_acceptnegstep, reg_min, ...) are attributes as
+on crocoddyl.SolverBoxFDDP; setCallbacks([CallbackVerbose()]) prints the
+per-iteration record of instance 0 after each solve (ffddp.callbacks).
 """
 from __future__ import annotations
 
@@ -24,9 +28,22 @@ class FfddpError(RuntimeError):
     pass
 
 
+_PARAMS = ("th_stop", "th_grad", "th_acceptstep", "th_acceptnegstep", "th_stepdec", "th_stepinc", "reg_min",
+           "reg_max", "reg_incfactor", "reg_decfactor", "neg_step_rule")
+
+
 class BatchedBoxFDDP:
-    def __init__(self, cfg: OcpConfig, max_batch: int, device: int = 0):
+    def __init__(self, cfg: OcpConfig, max_batch: int, device: int = 0, pinned_outputs: bool = False):
+        """pinned_outputs: solve() writes xs / us / K / ... into page-locked
+        arrays owned by the solver (copied by DMA as each slice finishes)
+        and returns views of them, overwritten by the next solve() -- copy
+        what must outlive it, as the reference does (crocoddyl_classical.py:
+        382-385).  Default: fresh arrays per solve()."""
         self.cfg = cfg
+        self.pinned_outputs = bool(pinned_outputs)
+        self._pin = {}
+        self._callbacks = []
+        self._trace_it = 0
         self.N = int(cfg.horizon)
         self.nx = cfg.nx
         self.nu = 7
@@ -41,6 +58,61 @@ class BatchedBoxFDDP:
             raise FfddpError(f"ffddp_create failed with code {rc}")
         self._h = h
         self.xs = self.us = self.K = self.cost = self.iter = self.ok = self.fn_pred = self.stats = None
+
+    # -- solver properties (crocoddyl SolverFDDP / SolverBoxFDDP attributes) ----------
+    @property
+    def solver_params(self) -> _abi.SolverParams:
+        p = _abi.SolverParams()
+        self._check(self._lib.ffddp_get_solver_params(self._h, C.byref(p)), "ffddp_get_solver_params")
+        return p
+
+    @solver_params.setter
+    def solver_params(self, p: _abi.SolverParams):
+        self._check(self._lib.ffddp_set_solver_params(self._h, C.byref(p)), "ffddp_set_solver_params")
+
+    def __getattr__(self, name):
+        if name in _PARAMS:
+            return getattr(self.solver_params, name)
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        if name in _PARAMS:
+            p = self.solver_params
+            setattr(p, name, value)
+            self.solver_params = p
+        else:
+            object.__setattr__(self, name, value)
+
+    # -- callbacks / per-iteration trace ------------------------------------------------
+    def setCallbacks(self, callbacks, max_iters: int = 64):
+        """crocoddyl solver.setCallbacks (crocoddyl_classical.py:353): the device
+        keeps a per-iteration record (include/ffddp.h ffddp_trace_*); every
+        callback is called with (solver, trace) after each solve."""
+        self._callbacks = list(callbacks)
+        self.trace_enable(max_iters if self._callbacks else 0)
+
+    def getCallbacks(self):
+        return list(self._callbacks)
+
+    def trace_enable(self, max_iters: int):
+        self._check(self._lib.ffddp_trace_enable(self._h, int(max_iters)), "ffddp_trace_enable")
+        self._trace_it = int(max_iters)
+
+    def trace(self, B: int | None = None) -> np.ndarray:
+        """[B][max_iters][TRACE_W] records of the last solve (NaN rows for
+        iterations an instance did not run); fields _abi.TRACE_FIELDS."""
+        if self._trace_it == 0:
+            raise FfddpError("trace not enabled (trace_enable / setCallbacks)")
+        B = int(self.cost.shape[0]) if B is None else int(B)
+        out = np.zeros((B, self._trace_it, _abi.TRACE_W))
+        self._check(self._lib.ffddp_trace_read(self._h, B, _abi.dptr(out)), "ffddp_trace_read")
+        return out
+
+    def _run_callbacks(self, B):
+        if self._callbacks:
+            tr = self.trace(B)
+            for cb in self._callbacks:
+                cb(self, tr)
 
     # -- lifecycle ------------------------------------------------------------------
     def close(self):
@@ -72,14 +144,16 @@ class BatchedBoxFDDP:
         surf = np.ascontiguousarray(np.asarray(batch.surface, np.uint8).reshape(B))
         xsi = f(batch.xs_init if xs_init is None else xs_init, (B, N + 1, nx))
         usi = f(batch.us_init if us_init is None else us_init, (B, N, 7))
-        xs = np.zeros((B, N + 1, nx))
-        us = np.zeros((B, N, 7))
-        K = np.zeros((B, N, 7, nx))
-        cost = np.zeros(B)
-        iters = np.zeros(B, np.int32)
-        ok = np.zeros(B, np.uint8)
-        fn = np.zeros((B, 2))
-        stats = np.zeros((B, _abi.NSTATS), np.int32)
+        specs = dict(xs=((B, N + 1, nx), np.float64), us=((B, N, 7), np.float64), K=((B, N, 7, nx), np.float64),
+                     cost=((B,), np.float64), iters=((B,), np.int32), ok=((B,), np.uint8), fn=((B, 2), np.float64),
+                     stats=((B, _abi.NSTATS), np.int32))
+        if self.pinned_outputs:
+            if B not in self._pin:
+                self._pin = {B: _abi.pinned_arrays(specs)}
+            o = self._pin[B]
+        else:
+            o = {k: np.zeros(shape, dt) for k, (shape, dt) in specs.items()}
+        xs, us, K, cost, iters, ok, fn, stats = (o[k] for k in ("xs", "us", "K", "cost", "iters", "ok", "fn", "stats"))
         d, i, u = _abi.dptr, _abi.iptr, _abi.uptr
         rc = self._lib.ffddp_solve_batch(
             self._h, B, d(x0), d(nref), d(iref), u(surf), d(xsi), d(usi), int(maxiter), int(bool(is_feasible)),
@@ -88,6 +162,7 @@ class BatchedBoxFDDP:
         self._check(rc, "ffddp_solve_batch")
         self.xs, self.us, self.K, self.cost, self.iter = xs, us, K, cost, iters
         self.ok, self.fn_pred, self.stats = ok.astype(bool), fn, stats
+        self._run_callbacks(B)
         return self.ok
 
     # -- solve (device-resident torch tensors; bench path) ---------------------------

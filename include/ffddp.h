@@ -22,6 +22,7 @@
 #ifndef FFDDP_H_
 #define FFDDP_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -176,12 +177,66 @@ int ffddp_calc_diff(ffddp_handle* h, int B, const double* x0, const double* node
 int ffddp_frame_placement(const ffddp_robot* robot, const double* q, double* R, double* p);
 int ffddp_gravity_torque(const ffddp_robot* robot, int B, const double* q, double* tau);
 
+/* Solver properties of crocoddyl.SolverBoxFDDP / SolverFDDP (the attributes
+ * the reference leaves at their defaults: th_stop, th_grad, th_acceptstep,
+ * th_acceptnegstep, th_stepdec, th_stepinc, reg_min/reg_max/reg_incfactor/
+ * reg_decfactor; crocoddyl_classical.py:442-445 constructs the solver and
+ * sets none of them).  neg_step_rule selects the comparator of the
+ * ascent-direction acceptance (dVexp < 0, only while infeasible,
+ * SolverFDDP::solve):
+ *   FFDDP_NEGSTEP_CROCODDYL     accept iff dV < th_acceptnegstep * dVexp
+ *                               (Crocoddyl's source; default)
+ *   FFDDP_NEGSTEP_BOUNDED_RISE  accept iff dV > th_acceptnegstep * dVexp
+ *                               (a rise of at most th_acceptnegstep x the
+ *                               predicted one; accepts the exact LQR step)
+ * Values set here apply to the following solves of the handle. */
+enum { FFDDP_NEGSTEP_CROCODDYL = 0, FFDDP_NEGSTEP_BOUNDED_RISE = 1 };
+typedef struct ffddp_solver_params {
+  double th_stop;          /* SolverBoxFDDP 5e-5, SolverFDDP 1e-9 */
+  double th_grad;          /* 1e-12 */
+  double th_acceptstep;    /* 0.1 */
+  double th_acceptnegstep; /* 2.0 */
+  double th_stepdec;       /* 0.5 */
+  double th_stepinc;       /* 0.01 */
+  double reg_min, reg_max; /* 1e-9, 1e9 */
+  double reg_incfactor, reg_decfactor; /* 10, 10 */
+  int32_t neg_step_rule;   /* FFDDP_NEGSTEP_* */
+  int32_t reserved;
+} ffddp_solver_params;
+int ffddp_get_solver_params(const ffddp_handle* h, ffddp_solver_params* p);
+int ffddp_set_solver_params(ffddp_handle* h, const ffddp_solver_params* p);
+
+/* Per-iteration solver trace: what crocoddyl.CallbackVerbose prints at the end
+ * of every iteration (solver.setCallbacks([crocoddyl.CallbackVerbose()]),
+ * crocoddyl_classical.py:352-353, 360-361; FF :588-599).  ffddp_trace_enable
+ * (h, max_iters) keeps a record per instance and iteration for the next solves
+ * (0 = off); ffddp_trace_read copies the last solve's records for its B
+ * instances to out [B][max_iters][FFDDP_TRACE_W] (host pointer):
+ *   [0] iter, [1] cost, [2] stop = sum ||Qu||^2, [3] grad = -d1 of the last
+ *   tried step length, [4] preg, [5] dreg (= preg), [6] step length (the
+ *   accepted one, else the smallest tried), [7] ||ffeas|| = max |fs| of the
+ *   iteration's calcDiff, [8] dV, [9] dV_exp of that step length.
+ * Iterations an instance did not reach (stopped earlier, failed backward
+ * pass) hold NaN rows. */
+#define FFDDP_TRACE_W 10
+int ffddp_trace_enable(ffddp_handle* h, int max_iters);
+int ffddp_trace_read(ffddp_handle* h, int B, double* out);
+
+/* Page-locked host memory for the host-pointer entry points: arrays passed to
+ * ffddp_solve_batch that live in such memory are copied by DMA on the slice
+ * streams, overlapping the other slices' kernels; pageable arrays go through
+ * the handle's own page-locked staging buffers. */
+int ffddp_host_alloc(size_t bytes, void** p);
+int ffddp_host_free(void* p);
+
 /* Optional per-kernel device timing (HIP events recorded around every launch
  * on the launch stream), one kernel per class.  Classes, in order: init,
  * node (calc + calcDiff tangents + Gauss-Newton, one fused kernel), backward,
- * forward (line search, first pass), accept (acceptance + copy of the accepted
- * trial), commit (unused), finalize, forward2 (line search, second pass),
- * primal (unused: the calc runs inside the node kernel).
+ * forward (line search, first pass), accept (acceptance test, regularisation,
+ * stopping; no copy: the next node kernel reads the accepted trial in place),
+ * commit (end of solve: accepted trials no node kernel consumed become
+ * xs / us), finalize, forward2 (line search, second pass), primal (unused:
+ * the calc runs inside the node kernel).
  * `classes` is a bit mask over those classes (bit i = class i; 0 = off,
  * FFDDP_PROFILE_ALL = every class).  Timing only the kernel of interest keeps
  * the event overhead out of the other launches.

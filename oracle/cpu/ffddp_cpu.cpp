@@ -547,7 +547,8 @@ bool solve_one(const DevConsts& C, Inst& I, int maxiter, int& iter_out) {
       const double d0 = I.dg + dvv, d1 = I.dq - 2.0 * dvv;
       const double dVexp = steplength * (d0 + 0.5 * steplength * d1);
       const bool ok = dVexp >= 0 ? (std::fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp)
-                                 : (!I.feas && dV > C.th_acceptnegstep * dVexp);
+                                 : (!I.feas && (C.neg_rule == FFDDP_NEGSTEP_CROCODDYL ? dV < C.th_acceptnegstep * dVexp
+                                                                                       : dV > C.th_acceptnegstep * dVexp));
       if (ok) {
         was_feasible = I.feas;
         I.xs.swap(I.xs_try);
@@ -620,17 +621,31 @@ int solve_batch_t(const DevConsts& C, int B, const double* x0, const double* nre
 extern "C" {
 
 // Same arguments and outputs as ffddp_solve_batch (include/ffddp.h) on host
-// arrays, plus the OpenMP thread count (<= 0: all the process may use).
+// arrays, plus the solver properties (ffddp_solver_params, NULL = defaults)
+// and the OpenMP thread count (<= 0: all the process may use).
 int ffddp_cpu_solve_batch(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int B, const double* x0,
                           const double* node_ref, const double* inst_ref, const uint8_t* surface,
                           const double* xs_init, const double* us_init, int maxiter, int is_feasible, double* xs,
                           double* us, double* K, double* cost, int32_t* iters, uint8_t* ok, int32_t* stats,
-                          int nthreads) {
+                          const ffddp_solver_params* sp, int nthreads) {
   if (!robot || !cfg || B < 0 || maxiter < 0) return FFDDP_E_INVALID;
   if (cfg->nc != 1 && cfg->nc != 3) return FFDDP_E_INVALID;
   if (B == 0) return 0;
   DevConsts C;
   fill_consts(*robot, *cfg, C);
+  if (sp) {
+    C.th_stop = sp->th_stop;
+    C.th_grad = sp->th_grad;
+    C.th_acceptstep = sp->th_acceptstep;
+    C.th_acceptnegstep = sp->th_acceptnegstep;
+    C.th_stepdec = sp->th_stepdec;
+    C.th_stepinc = sp->th_stepinc;
+    C.reg_min = sp->reg_min;
+    C.reg_max = sp->reg_max;
+    C.reg_inc = sp->reg_incfactor;
+    C.reg_dec = sp->reg_decfactor;
+    C.neg_rule = sp->neg_step_rule;
+  }
   const bool ff = cfg->variant == FFDDP_FORCE_FEEDBACK;
 #define FFDDP_CPU(NC_, FF_) \
   solve_batch_t<NC_, FF_>(C, B, x0, node_ref, inst_ref, surface, xs_init, us_init, maxiter, is_feasible, xs, us, K, cost, iters, ok, stats, nthreads)

@@ -28,7 +28,7 @@ def load():
         lib = C.CDLL(str(LIB))
         dp, ip, up, vp = C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_uint8), C.c_void_p
         lib.ffddp_cpu_solve_batch.argtypes = [vp, vp, C.c_int, dp, dp, dp, up, dp, dp, C.c_int, C.c_int,
-                                              dp, dp, dp, dp, ip, up, ip, C.c_int]
+                                              dp, dp, dp, dp, ip, up, ip, vp, C.c_int]
         lib.ffddp_cpu_solve_batch.restype = C.c_int
         lib.ffddp_cpu_max_threads.restype = C.c_int
         _lib = lib
@@ -36,10 +36,11 @@ def load():
 
 
 def solve_batch(robot_struct, cfg_struct, batch, maxiter=10, is_feasible=False, nthreads=0, xs_init=None,
-                us_init=None):
+                us_init=None, solver_params=None):
     """robot_struct / cfg_struct: ctypes ffddp_robot / ffddp_ocp_config
-    (ffddp._abi.Robot / OcpConfig); batch: workload.Batch.  Returns a dict
-    with xs, us, K, cost, iter, ok, stats (numpy)."""
+    (ffddp._abi.Robot / OcpConfig); batch: workload.Batch; solver_params: an
+    _abi.SolverParams (None = the defaults).  Returns a dict with xs, us, K,
+    cost, iter, ok, stats (numpy)."""
     lib = load()
     B = int(batch.x0.shape[0])
     N = int(cfg_struct.horizon)
@@ -59,7 +60,7 @@ def solve_batch(robot_struct, cfg_struct, batch, maxiter=10, is_feasible=False, 
     rc = lib.ffddp_cpu_solve_batch(C.byref(robot_struct), C.byref(cfg_struct), B, d(x0), d(nref), d(iref), u8(surf),
                                    d(xsi), d(usi), int(maxiter), int(bool(is_feasible)), d(out["xs"]), d(out["us"]),
                                    d(out["K"]), d(out["cost"]), i32(out["iter"]), u8(out["ok"]), i32(out["stats"]),
-                                   int(nthreads))
+                                   C.byref(solver_params) if solver_params is not None else None, int(nthreads))
     if rc != 0:
         raise RuntimeError(f"ffddp_cpu_solve_batch failed ({rc})")
     out["ok"] = out["ok"].astype(bool)

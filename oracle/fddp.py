@@ -38,6 +38,9 @@ class Consts:
     th_grad: float = 1e-12
     th_acceptstep: float = 0.1
     th_acceptnegstep: float = 2.0
+    # ascent-direction comparator (include/ffddp.h FFDDP_NEGSTEP_*):
+    # 0 = Crocoddyl's `dV < th_acceptnegstep * dVexp`, 1 = bounded rise `>`
+    neg_step_rule: int = 0
     th_stepdec: float = 0.5
     th_stepinc: float = 0.01
     reg_min: float = 1e-9
@@ -122,18 +125,23 @@ def boxqp(H, q, lb, ub, xinit, c: Consts):
 
 
 def accept_step(c: Consts, is_feasible: bool, dV: float, d0: float, dVexp: float) -> bool:
-    """SolverFDDP::solve step acceptance for one trial.
-    Descent direction (dVexp >= 0): Armijo-like, |d0| < th_grad or
-    dV > th_acceptstep dVexp.  Ascent direction (dVexp < 0, closing the gaps
-    may raise the cost): Crocoddyl 2.x takes this branch only while infeasible
-    (`!is_feasible_ && ...`) and accepts a rise of up to th_acceptnegstep x the
-    predicted one (dV > 2 dVexp, both negative).  SURVEY.md B.1 writes
-    "dV < 2 dVexp"; that rejects the exact LQR step (see
-    tests/test_oracle.py::test_fddp_lqr_known_answer) and DESIGN.md §3 records
-    the choice.  The HIP kernel's trial_accepted is the same rule."""
+    """SolverFDDP::solve step acceptance for one trial (SURVEY.md Appendix B.1).
+    Descent direction (dVexp >= 0): |d0| < th_grad or dV > th_acceptstep dVexp.
+    Ascent direction (dVexp < 0, closing the gaps may raise the cost): only
+    while infeasible (`!is_feasible_ && ...`), with Crocoddyl's comparator
+    `dV < th_acceptnegstep * dVexp` (neg_step_rule 0, the default), or the
+    bounded-rise alternative `dV > th_acceptnegstep * dVexp` (rule 1: a rise
+    of at most th_acceptnegstep x the predicted one; the only one of the two
+    that accepts the exact LQR step whose cost must rise, see
+    tests/test_oracle.py::test_fddp_lqr_known_answer).  The HIP kernel's
+    trial_accepted and oracle/cpu implement the same switch."""
     if dVexp >= 0:
         return abs(d0) < c.th_grad or dV > c.th_acceptstep * dVexp
-    return (not is_feasible) and dV > c.th_acceptnegstep * dVexp
+    if is_feasible:
+        return False
+    if c.neg_step_rule == 0:
+        return dV < c.th_acceptnegstep * dVexp
+    return dV > c.th_acceptnegstep * dVexp
 
 
 @dataclass
@@ -143,6 +151,7 @@ class Stats:
     reg_retries: int = 0
     forward_errors: int = 0  # line-search trials rejected as non-finite (raiseIfNaN)
     neg_branch: int = 0  # trials judged by the ascent-direction (dVexp < 0) branch
+    neg_accepted: int = 0  # ... and accepted by it
     clamped: int = 0  # BoxQP solutions with at least one active bound
 
 
@@ -177,6 +186,7 @@ class SolverBoxFDDP:
         if not self.is_feasible:
             self.fs[0] = self.x0 - self.xs[0]
             self.fs[1:] = run["xnext"] - self.xs[1:]
+        self.ffeas = float(np.max(np.abs(self.fs)))  # ||ffeas||_inf of this calcDiff
 
     def _backward(self):
         N, c = self.N, self.c
@@ -298,6 +308,10 @@ class SolverBoxFDDP:
         self.K = np.zeros((self.N, self.nu, self.nx))
         self.stats = Stats()
         self.stop = float("nan")
+        # CallbackVerbose records (include/ffddp.h ffddp_trace_*): iter, cost,
+        # stop, grad = -d1, preg, dreg, step, ffeas, dV, dVexp
+        self.trace = []
+        self.ffeas = 0.0
         recalc = True
         self.iter = 0
         for it in range(maxiter):
@@ -318,6 +332,7 @@ class SolverBoxFDDP:
                 break
             self._update_expected_improvement()
             steplength = c.alphas[0]
+            tdV = tdVexp = td1 = float("nan")
             for steplength in c.alphas:
                 self.stats.trials += 1
                 try:
@@ -328,9 +343,12 @@ class SolverBoxFDDP:
                 dV = self.cost - cost_try
                 d0, d1 = self._expected_improvement(xs_try)
                 dVexp = steplength * (d0 + 0.5 * steplength * d1)
+                tdV, tdVexp, td1 = dV, dVexp, d1
                 if dVexp < 0:
                     self.stats.neg_branch += 1
                 ok = accept_step(c, self.is_feasible, dV, d0, dVexp)
+                if ok and dVexp < 0:
+                    self.stats.neg_accepted += 1
                 if ok:
                     self.was_feasible = self.is_feasible
                     self.xs, self.us = xs_try, us_try
@@ -345,6 +363,7 @@ class SolverBoxFDDP:
                 if self.preg == c.reg_max:
                     return False
             self.stop = float(np.sum(self.Qu * self.Qu))
+            self.trace.append((it, self.cost, self.stop, -td1, self.preg, self.preg, steplength, self.ffeas, tdV, tdVexp))
             if self.was_feasible and self.stop < self.th_stop:
                 return True
         self.iter = maxiter

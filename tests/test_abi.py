@@ -38,6 +38,9 @@ def test_struct_layout_matches_header():
 int main(void) {
   printf("%zu %zu %zu %zu %d ", sizeof(ffddp_plant_params), offsetof(ffddp_plant_params, armature),
          offsetof(ffddp_plant_params, r_tool), offsetof(ffddp_plant_params, site_R), FFDDP_PLANT_OBS);
+  printf("%zu %zu %zu %d %d %d ", sizeof(ffddp_solver_params), offsetof(ffddp_solver_params, reg_decfactor),
+         offsetof(ffddp_solver_params, neg_step_rule), FFDDP_TRACE_W, FFDDP_NEGSTEP_CROCODDYL,
+         FFDDP_NEGSTEP_BOUNDED_RISE);
   printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(ffddp_robot), sizeof(ffddp_ocp_config),
          offsetof(ffddp_ocp_config, dt), offsetof(ffddp_ocp_config, R_des),
          offsetof(ffddp_ocp_config, y_weights), offsetof(ffddp_ocp_config, use_inner_tau_reg),
@@ -55,6 +58,11 @@ int main(void) {
     Pp = _abi.PlantParams
     assert vals[:5] == [ctypes.sizeof(Pp), Pp.armature.offset, Pp.r_tool.offset, Pp.site_R.offset, _abi.PLANT_OBS]
     vals = vals[5:]
+    Sp = _abi.SolverParams
+    assert vals[:6] == [ctypes.sizeof(Sp), Sp.reg_decfactor.offset, Sp.neg_step_rule.offset, _abi.TRACE_W,
+                        _abi.NEGSTEP_CROCODDYL, _abi.NEGSTEP_BOUNDED_RISE]
+    assert len(_abi.TRACE_FIELDS) == _abi.TRACE_W
+    vals = vals[6:]
     assert vals == [
         ctypes.sizeof(_abi.Robot), ctypes.sizeof(C), C.dt.offset, C.R_des.offset, C.y_weights.offset,
         C.use_inner_tau_reg.offset, ctypes.sizeof(_abi.Task), _abi.Task.has_ee_start.offset, _abi.Task.q_nom.offset,
@@ -90,6 +98,28 @@ def test_null_handle_errors():
     lib = _abi.load()
     assert lib.ffddp_profile_enable(None, 1) == -1
     assert b"null" in lib.ffddp_last_error(None)
+    p = _abi.solver_params()
+    assert lib.ffddp_get_solver_params(None, ctypes.byref(p)) == -1
+    assert lib.ffddp_set_solver_params(None, ctypes.byref(p)) == -1
+    assert lib.ffddp_trace_enable(None, 4) == -1
+    assert lib.ffddp_trace_read(None, 1, None) == -1
+    assert lib.ffddp_host_alloc(16, None) == -1
+    assert lib.ffddp_host_free(None) == 0
+
+
+def test_solver_param_defaults_match_oracle():
+    """The library's SolverBoxFDDP defaults (mirrored by _abi.solver_params)
+    are the oracle's constants (oracle/fddp.py Consts)."""
+    from oracle import fddp
+
+    c, p = fddp.Consts(), _abi.solver_params()
+    assert p.th_stop == c.th_stop_box and _abi.solver_params(use_box=False).th_stop == c.th_stop_fddp
+    for k in ("th_grad", "th_acceptstep", "th_acceptnegstep", "th_stepdec", "th_stepinc", "reg_min", "reg_max",
+              "reg_incfactor", "reg_decfactor", "neg_step_rule"):
+        assert getattr(p, k) == getattr(c, k), k
+    hdr = HEADER.read_text()
+    for k, v in (("th_stop", "5e-5"), ("th_grad", "1e-12"), ("th_acceptnegstep", "2.0")):
+        assert re.search(rf"double {k};\s*/\*[^*]*{re.escape(v)}", hdr), k
 
 
 def test_integration_snippet_matches_header():

@@ -10,7 +10,7 @@ import pytest
 
 from ffddp import _abi
 from helpers import make_batch, product_cfg, rel_err
-from oracle import cpu_fddp
+from oracle import cpu_fddp, fddp
 from oracle_pool import solve_many
 
 CASES = [
@@ -51,8 +51,13 @@ def test_cpu_baseline_exceptional_paths():
         else:
             b.x0 = b.x0.copy()
             b.x0[:, 7:] += 50.0
-        out = cpu_fddp.solve_batch(_abi.robot_struct(), cfg.to_struct(), b, nthreads=2)
-        ref = solve_many(cfg, b, range(B))
+        # nan: the bounded-rise ascent comparator; Crocoddyl's (dV < 2 dVexp)
+        # accepts this start's first gap-closing step at a cost of ~1e24, where
+        # two fp64 implementations no longer agree to 1e-9
+        rule = _abi.NEGSTEP_BOUNDED_RISE if tweak == "nan" else _abi.NEGSTEP_CROCODDYL
+        out = cpu_fddp.solve_batch(_abi.robot_struct(), cfg.to_struct(), b, nthreads=2,
+                                   solver_params=_abi.solver_params(neg_step_rule=rule))
+        ref = solve_many(cfg, b, range(B), consts=fddp.Consts(neg_step_rule=rule))
         key = {"clamp": "clamped", "retry": "reg_retries", "nan": "forward_errors"}[tweak]
         assert all(r[key] > 0 for r in ref)
         for i, r in enumerate(ref):

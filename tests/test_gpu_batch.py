@@ -71,6 +71,25 @@ def test_full_batch_equals_small_batches(variant, B, monkeypatch):
     small.close()
 
 
+def test_pinned_outputs_bit_identical():
+    """Host entry point with page-locked caller arrays (DMA per slice, no
+    staging) vs pageable ones (staging buffer + host copies): same bits."""
+    N, B = 30, 1030
+    cfg = product_cfg("classical", N)
+    batch = make_batch("classical", B, N, seed=78)
+    a = BatchedBoxFDDP(cfg, max_batch=B)
+    a.solve(batch, maxiter=10)
+    p = BatchedBoxFDDP(cfg, max_batch=B, pinned_outputs=True)
+    p.solve(batch, maxiter=10)
+    for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred", "stats"):
+        assert np.array_equal(getattr(a, name), getattr(p, name), equal_nan=True), name
+    first = p.xs
+    p.solve(batch.slice(slice(0, B)), maxiter=10)  # same buffers, overwritten in place
+    assert p.xs is first
+    a.close()
+    p.close()
+
+
 def test_feasible_warm_start_matches_oracle():
     """is_feasible = True: xs_init is the rollout of us_init (gravity torques)
     through the dynamics, so the guess has no gaps (SolverFDDP feasible start)."""

@@ -1,0 +1,103 @@
+"""GPU: the two BASELINE configs the parity cases do not otherwise run at size.
+
+* configs[3] — all 5 scenarios x 256 seeds = 1280 closed loops
+  (run_classical.py:30-39 seeds, :53-91 scenarios) as one fleet on one GPU,
+  1.0 s each (200 ticks: through the contact onset at 0.8 s and the 0.2 s
+  hold).  Per-instance properties (finite torques, tracking error and force
+  bounds in every scenario) and three instances from different scenarios
+  replayed tick for tick through the scalar ClassicalCrocoddylMPC (B = 1
+  solves, ffddp.controller) at 1e-7.
+* configs[4] per-GPU shape — horizon 100, point3d, B = 1024 (the 8192-instance
+  batch over 8 GPUs): every checked instance equals, bit for bit, the same
+  instance solved in a batch of 8 on one stream, and a spread of them
+  matches the oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from ffddp import BatchedBoxFDDP  # noqa: E402
+from ffddp import controller as CT  # noqa: E402
+from ffddp import fleet as FL  # noqa: E402
+from ffddp import plant as PL  # noqa: E402
+
+from helpers import log_parity, make_batch, product_cfg, rel_err  # noqa: E402
+from oracle_pool import solve_many  # noqa: E402
+
+
+def test_c4_full_sweep_1280_instances():
+    seeds = 256
+    rec = [0, 2 * seeds + 5, 4 * seeds + 7]  # flat, tilted_10, actuation_uncertainty
+    out = FL.run_sweep(seeds=seeds, total_time=1.0, verbose=False, record=rec)
+    assert out["instances"] == 1280 and out["n_all"] == 1280 and out["ticks"] == 200
+    names = out["names"]
+    assert [int(np.sum(names == s)) for s in dict.fromkeys(names)] == [seeds] * 5
+    pi = out["per_instance"]
+    for k in ("rms_3d_error", "rms_tangential_error", "max_fn"):
+        assert np.all(np.isfinite(pi[k])), k
+    # every loop tracks the approach and presses without blowing up
+    assert np.max(pi["rms_3d_error"]) < 0.1 and np.median(pi["rms_3d_error"]) < 0.05
+    assert np.max(pi["max_fn"]) < 500.0
+    for s in dict.fromkeys(names):
+        sel = names == s
+        assert np.median(pi["rms_3d_error"][sel]) < 0.05, s
+    r = out["record"]
+    assert np.all(np.isfinite(r["tau"]))
+    worst = 0.0
+    for j, b in enumerate(r["index"]):
+        sim = PL.PandaTablePlant(n_substeps=5, timestep=0.001)
+        sim.set_state(r["q0"][j])
+        ctrl = CT.ClassicalCrocoddylMPC(sim=sim, traj_fn=r["traj"], config=r["config"])
+        for k in range(out["ticks"]):
+            tau_s = ctrl.compute_control(PL.observation_from_record(r["obs"][k, j]), float(r["t"][k]))
+            np.testing.assert_allclose(r["tau"][k, j], tau_s, rtol=1e-7, atol=1e-7, err_msg=f"instance {b} tick {k}")
+            worst = max(worst, float(np.max(np.abs(r["tau"][k, j] - tau_s))))
+        ctrl.close()
+        sim.close()
+    log_parity("c4_sweep/1280/replay3", worst_tau=worst, ticks=out["ticks"], wall_s=out["wall_s"])
+
+
+def _sub(batch, idx):
+    import copy
+
+    b = copy.copy(batch)
+    for f in ("x0", "node_ref", "inst_ref", "surface", "xs_init", "us_init", "t0"):
+        setattr(b, f, np.ascontiguousarray(getattr(batch, f)[idx]))
+    return b
+
+
+def test_c5_per_gpu_shape_point3d_n100(monkeypatch):
+    N, B = 100, 1024
+    cfg = product_cfg("classical", N, "point3d")
+    batch = make_batch("classical", B, N, seed=505, surface=1)
+    big = BatchedBoxFDDP(cfg, max_batch=B)
+    big.solve(batch, maxiter=10)
+    assert np.all(np.isfinite(big.cost))
+    monkeypatch.setenv("FFDDP_STREAMS", "1")
+    small = BatchedBoxFDDP(cfg, max_batch=8)
+    rng = np.random.default_rng(2)
+    picks = np.unique(np.concatenate([[0, 1, B // 4 - 1, B // 4, B // 2, B - 1], rng.integers(0, B, 10)]))
+    for i0 in range(0, len(picks), 8):
+        idx = picks[i0:i0 + 8]
+        small.solve(_sub(batch, idx), maxiter=10)
+        for j, i in enumerate(idx):
+            for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred", "stats"):
+                a, b = getattr(big, name)[i], getattr(small, name)[j]
+                assert np.array_equal(a, b, equal_nan=True), (name, int(i))
+    sel = picks[::2]
+    ref = solve_many(cfg, batch, sel)
+    e = dict(xs=0.0, us=0.0, K=0.0, cost=0.0)
+    for i, r in zip(sel, ref):
+        assert bool(big.ok[i]) == r["ok"] and int(big.iter[i]) == r["iter"]
+        assert int(big.stats[i, 1]) == r["trials"]
+        for k in ("xs", "us", "K"):
+            e[k] = max(e[k], rel_err(getattr(big, k)[i], r[k]))
+        e["cost"] = max(e["cost"], rel_err(big.cost[i], r["cost"]))
+    log_parity(f"batch/point3d/N{N}/B{B}", n=len(sel), **e)
+    # point3d / N = 100 error budget: tests/test_gpu_parity.py CASE_TOL
+    assert max(e["xs"], e["us"], e["cost"]) < 6e-7 and e["K"] < 2e-6, e
+    big.close()
+    small.close()

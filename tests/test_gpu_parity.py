@@ -20,8 +20,8 @@ friction cone, the SURVEY-literal random x0 at N = 30, plain FDDP and N = 100.
 import numpy as np
 import pytest
 
-from ffddp import BatchedBoxFDDP
-from oracle import ocp
+from ffddp import BatchedBoxFDDP, _abi
+from oracle import fddp, ocp
 
 from helpers import log_parity, make_batch, oracle_cfg, oracle_problem, product_cfg, rel_err
 from oracle_pool import solve_many
@@ -181,21 +181,112 @@ def test_solve_backward_failures_retry():
     _check_solves("solve/backward_retries", cfg, b, solver, ref)
 
 
-def test_solve_nonfinite_line_search_trials():
-    """x0 with a 50 rad/s velocity offset and an xs_init[0] that does not
-    contain it: the alpha = 1 rollout starts at x0 and overflows (raiseIfNaN:
-    the trial is rejected), shorter steps stay finite."""
-    N, B = 12, 4
+def _nonfinite_case(N=12, B=4):
     cfg = product_cfg("classical", N)
     b = make_batch("classical", B, N, seed=21, surface=1)
     b.x0 = b.x0.copy()
     b.x0[:, 7:] += 50.0
+    return cfg, b
+
+
+def test_solve_nonfinite_line_search_trials():
+    """x0 with a 50 rad/s velocity offset and an xs_init[0] that does not
+    contain it: the alpha = 1 rollout starts at x0 and overflows (raiseIfNaN:
+    the trial is rejected), shorter steps stay finite.  Bounded-rise ascent
+    comparator on both sides (FFDDP_NEGSTEP_BOUNDED_RISE): the gap-closing
+    steps raise the cost and are accepted while the rise stays within 2x the
+    predicted one."""
+    cfg, b = _nonfinite_case()
+    B = b.B
     solver = BatchedBoxFDDP(cfg, max_batch=B)
+    solver.neg_step_rule = _abi.NEGSTEP_BOUNDED_RISE
+    assert solver.neg_step_rule == _abi.NEGSTEP_BOUNDED_RISE
     solver.solve(b, maxiter=10, is_feasible=False)
-    ref = solve_many(cfg, b, range(B))
+    ref = solve_many(cfg, b, range(B), consts=fddp.Consts(neg_step_rule=1))
     assert all(r["forward_errors"] > 0 for r in ref)
     totals = _check_solves("solve/nonfinite_trials", cfg, b, solver, ref, tol=1.5e-9, tol_k=TOL_K)
     assert totals["neg_branch"] > 0
+    assert sum(r["neg_accepted"] for r in ref) > 0
+
+
+def test_ascent_branch_crocoddyl_comparator():
+    """The same start under Crocoddyl's comparator (dV < 2 dVexp, the
+    default): the first iteration accepts a gap-closing step whose cost rises
+    by far more than predicted (to ~1e16..1e24), after which the two fp64
+    implementations can no longer be compared value for value; the discrete
+    path (step lengths, iterations, ok, trials) and the accepted step's
+    predicted change must still agree."""
+    cfg, b = _nonfinite_case()
+    B = b.B
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    assert solver.neg_step_rule == _abi.NEGSTEP_CROCODDYL
+    solver.trace_enable(10)
+    solver.solve(b, maxiter=10, is_feasible=False)
+    tr = solver.trace()
+    ref = solve_many(cfg, b, range(B))
+    assert sum(r["neg_accepted"] for r in ref) > 0
+    for i, r in enumerate(ref):
+        assert bool(solver.ok[i]) == r["ok"] and int(solver.iter[i]) == r["iter"]
+        assert int(solver.stats[i, 1]) == r["trials"] and int(solver.stats[i, 2]) == r["reg_retries"]
+        assert tr[i, 0, 6] == r["trace"][0, 6]  # accepted step length of iteration 0
+        assert abs(tr[i, 0, 9] - r["trace"][0, 9]) <= 1e-9 * abs(r["trace"][0, 9])  # its dV_exp
+    log_parity("solve/ascent_crocoddyl", B=B, neg_accepted=sum(r["neg_accepted"] for r in ref))
+
+
+def test_trace_matches_oracle():
+    """ffddp_trace_*: the per-iteration record CallbackVerbose prints (iter,
+    cost, stop, grad, preg, dreg, step, ffeas, dV, dV_exp) equals the
+    oracle's, iteration by iteration; iterations not run are NaN rows."""
+    N, B, it = 30, 4, 12
+    cfg = product_cfg("classical", N)
+    b = make_batch("classical", B, N, seed=23, surface=1, regime="random")
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    solver.trace_enable(it)
+    solver.solve(b, maxiter=10, is_feasible=False)
+    tr = solver.trace()
+    assert tr.shape == (B, it, _abi.TRACE_W)
+    ref = solve_many(cfg, b, range(B))
+    worst = 0.0
+    for i, r in enumerate(ref):
+        n = r["trace"].shape[0]
+        assert n >= 1 and np.all(np.isnan(tr[i, n:]))
+        g, o = tr[i, :n], r["trace"]
+        for col in (0, 4, 5, 6):  # iter, preg, dreg, step: exact
+            assert np.array_equal(g[:, col], o[:, col]), (i, _abi.TRACE_FIELDS[col])
+        for col in (1, 2, 3, 7, 8, 9):
+            e = float(np.max(np.abs(g[:, col] - o[:, col]) / np.maximum(1.0, np.abs(o[:, col]))))
+            worst = max(worst, e)
+            assert e < 1e-8, (i, _abi.TRACE_FIELDS[col], e)
+    log_parity("trace/classical/random", B=B, worst=worst)
+    # the CallbackVerbose replay of instance 0
+    from ffddp.callbacks import CallbackVerbose
+    import io
+
+    cb = CallbackVerbose(stream=io.StringIO())
+    solver.setCallbacks([cb], max_iters=it)
+    solver.solve(b, maxiter=10, is_feasible=False)
+    assert len(cb.lines) == ref[0]["trace"].shape[0] + 1  # one header (iteration 0) + one line per iteration
+
+
+def test_solver_params_apply():
+    """Solver properties set on the handle (crocoddyl solver attributes):
+    defaults as documented; a looser th_stop / stronger reg_min change the
+    solve exactly as they change the oracle's."""
+    N, B = 30, 4
+    cfg = product_cfg("classical", N)
+    b = make_batch("classical", B, N, seed=24, surface=1)
+    solver = BatchedBoxFDDP(cfg, max_batch=B)
+    d = _abi.solver_params()
+    p = solver.solver_params
+    for k, _ in _abi.SolverParams._fields_:
+        assert getattr(p, k) == getattr(d, k), k
+    solver.th_stop = 1e-2
+    solver.reg_min = 1e-6
+    solver.solve(b, maxiter=10, is_feasible=False)
+    ref = solve_many(cfg, b, range(B), consts=fddp.Consts(th_stop_box=1e-2, reg_min=1e-6))
+    _check_solves("solve/params/th_stop1e-2_regmin1e-6", cfg, b, solver, ref)
+    with pytest.raises(Exception):
+        solver.reg_min = -1.0
 
 
 def test_long_horizon_point3d_matches_oracle():
@@ -228,6 +319,42 @@ def test_gravity_torque_dev_matches_oracle():
     err = rel_err(td.cpu().numpy(), P.gravity_torque(q))
     log_parity("gravity_dev", err=err)
     assert err < 1e-12
+
+
+# Every launch setting the library reads (include/INTEGRATION.md §4): at
+# B = 520 (4 slices of 130, or 8 of 65) each setting gives, bit for bit, the
+# default schedule's solution -- the per-instance arithmetic does not depend
+# on slicing, stream placement, stagger, line-search pass split or backward
+# variant (the default schedule is itself checked against the oracle at
+# B = 4096 / 517 in tests/test_gpu_batch.py).
+ENV_VARIANTS = [
+    {"FFDDP_FW_SCHED": "1,3,5"}, {"FFDDP_FW_SCHED": "10"}, {"FFDDP_FW_FIRST": "1"}, {"FFDDP_STAGGER": "0"},
+    {"FFDDP_STAGGER": "1"}, {"FFDDP_CALLER_SLICE": "0"}, {"FFDDP_STREAMS": "2"}, {"FFDDP_STREAMS": "3"},
+    {"FFDDP_STREAMS": "8"}, {"FFDDP_BW_LATE_MAX": "0"}, {"FFDDP_BW_LATE_MAX": "100000"}, {"FFDDP_FW_FILL": "0"},
+]
+
+
+@pytest.mark.parametrize("variant", ["classical", "ff"])
+def test_launch_settings_bit_identical(variant, monkeypatch):
+    N, B = 30, 520
+    cfg = _cfg(variant, N, "normal_1d")
+    b = make_batch(variant, B, N, seed=31)
+    base = BatchedBoxFDDP(cfg, max_batch=B)
+    base.solve(b, maxiter=10, is_feasible=False)
+    names = ("xs", "us", "K", "cost", "iter", "ok", "fn_pred")
+    ref = {k: getattr(base, k).copy() for k in names}
+    ref_trials = base.stats[:, 1].copy()
+    base.close()
+    for env in ENV_VARIANTS:
+        with monkeypatch.context() as m:
+            for k, v in env.items():
+                m.setenv(k, v)  # read by ffddp_create
+            s = BatchedBoxFDDP(cfg, max_batch=B)
+        s.solve(b, maxiter=10, is_feasible=False)
+        for k in names:
+            assert np.array_equal(getattr(s, k), ref[k], equal_nan=True), (env, k)
+        assert np.array_equal(s.stats[:, 1], ref_trials), env
+        s.close()
 
 
 # Launch-schedule variants (the small parity batches otherwise always take

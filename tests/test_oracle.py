@@ -206,14 +206,24 @@ def _lqr_direct(m):
 
 def test_fddp_lqr_known_answer():
     """Linear dynamics + quadratic cost: the first full step closes the gaps and
-    lands on the optimum; the solver then stops (iter 1, ok)."""
+    lands on the optimum; the solver then stops (iter 1, ok).  Closing the
+    gaps of this LQR raises the cost (dVexp < 0) and the quadratic model is
+    exact (dV = dVexp), so the step is accepted only by the bounded-rise
+    comparator (neg_step_rule 1); Crocoddyl's own comparator
+    (dV < 2 dVexp) rejects it, and every shorter step too."""
     rng = np.random.default_rng(3)
     m = _lqr(rng)
     xs_ref, us_ref = _lqr_direct(m)
-    s = fddp.SolverBoxFDDP(m, box=False)
+    s = fddp.SolverBoxFDDP(m, box=False, consts=fddp.Consts(neg_step_rule=1))
     ok = s.solve(np.zeros((m.N + 1, m.nx)), np.zeros((m.N, m.nu)), maxiter=10)
     assert ok and s.iter == 1
     assert np.allclose(s.xs, xs_ref, atol=1e-10) and np.allclose(s.us, us_ref, atol=1e-10)
+    # the first iteration took the ascent branch with an exact model
+    it0 = s.trace[0]
+    assert it0[9] < 0 and abs(it0[8] - it0[9]) <= 1e-6 * abs(it0[9]) and it0[6] == 1.0
+    c = fddp.SolverBoxFDDP(m, box=False)
+    c.solve(np.zeros((m.N + 1, m.nx)), np.zeros((m.N, m.nu)), maxiter=1)
+    assert c.stats.neg_branch == 10 and not c.is_feasible  # every step length rejected
 
 
 def test_boxfddp_lqr_with_bounds_is_feasible_and_bounded():
@@ -222,7 +232,8 @@ def test_boxfddp_lqr_with_bounds_is_feasible_and_bounded():
     xs_ref, us_ref = _lqr_direct(m)
     bound = 0.5 * np.abs(us_ref).max()
     m.u_lb, m.u_ub = -bound * np.ones(m.nu), bound * np.ones(m.nu)
-    s = fddp.SolverBoxFDDP(m, box=True)
+    # closing this LQR's gaps raises the cost: bounded-rise comparator (see above)
+    s = fddp.SolverBoxFDDP(m, box=True, consts=fddp.Consts(neg_step_rule=1))
     s.solve(np.zeros((m.N + 1, m.nx)), np.zeros((m.N, m.nu)), maxiter=20)
     assert np.all(s.us <= bound + 1e-12) and np.all(s.us >= -bound - 1e-12)
     # dynamics satisfied (feasible rollout)
@@ -277,16 +288,22 @@ def test_backward_failure_raises_regularisation():
 
 def test_accept_step_rule():
     """SolverFDDP::solve acceptance (oracle.fddp.accept_step, the rule the HIP
-    kernel's trial_accepted implements)."""
+    kernel's trial_accepted implements), both ascent-branch comparators."""
     c = fddp.Consts()
+    assert c.neg_step_rule == 0  # Crocoddyl's comparator is the default
     # descent direction: sufficient decrease
     assert fddp.accept_step(c, False, dV=0.2, d0=1.0, dVexp=1.0)
     assert not fddp.accept_step(c, False, dV=0.05, d0=1.0, dVexp=1.0)
     assert fddp.accept_step(c, True, dV=-1.0, d0=1e-13, dVexp=1e-13)  # |d0| < th_grad
-    # ascent direction while infeasible: a rise of up to 2x the predicted one
-    assert fddp.accept_step(c, False, dV=-1.5, d0=-1.0, dVexp=-1.0)
-    assert not fddp.accept_step(c, False, dV=-2.5, d0=-1.0, dVexp=-1.0)
-    # ascent direction once feasible: never (Crocoddyl 2.x `!is_feasible_ && ...`),
-    # even for a trial that lowers the cost
-    assert not fddp.accept_step(c, True, dV=-0.5, d0=-1.0, dVexp=-1.0)
-    assert not fddp.accept_step(c, True, dV=+0.5, d0=-1.0, dVexp=-1.0)
+    # ascent direction while infeasible, Crocoddyl: dV < 2 dVexp
+    assert not fddp.accept_step(c, False, dV=-1.5, d0=-1.0, dVexp=-1.0)
+    assert fddp.accept_step(c, False, dV=-2.5, d0=-1.0, dVexp=-1.0)
+    # bounded rise: dV > 2 dVexp
+    b = fddp.Consts(neg_step_rule=1)
+    assert fddp.accept_step(b, False, dV=-1.5, d0=-1.0, dVexp=-1.0)
+    assert not fddp.accept_step(b, False, dV=-2.5, d0=-1.0, dVexp=-1.0)
+    # ascent direction once feasible: never (`!is_feasible_ && ...`), either rule
+    for cc in (c, b):
+        assert not fddp.accept_step(cc, True, dV=-0.5, d0=-1.0, dVexp=-1.0)
+        assert not fddp.accept_step(cc, True, dV=+0.5, d0=-1.0, dVexp=-1.0)
+        assert not fddp.accept_step(cc, True, dV=-2.5, d0=-1.0, dVexp=-1.0)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel-class sums of SQ counters from tools/pmc_sq.sh passes."""
+"""Per-kernel-class sums of SQ counters from tools/pmc_sq2.sh passes."""
 import csv, sys
 from collections import defaultdict
 from pathlib import Path
