@@ -228,18 +228,26 @@ def test_ascent_branch_crocoddyl_comparator():
     for i, r in enumerate(ref):
         assert bool(solver.ok[i]) == r["ok"] and int(solver.iter[i]) == r["iter"]
         assert int(solver.stats[i, 1]) == r["trials"] and int(solver.stats[i, 2]) == r["reg_retries"]
-        assert tr[i, 0, 6] == r["trace"][0, 6]  # accepted step length of iteration 0
-        assert abs(tr[i, 0, 9] - r["trace"][0, 9]) <= 1e-9 * abs(r["trace"][0, 9])  # its dV_exp
+        n = r["trace"].shape[0]
+        assert np.array_equal(tr[i, :n, 6], r["trace"][:, 6])  # step length of every iteration
+        # the accepted ascent step's predicted change (dVexp < 0): its dv term
+        # is a product with a rollout that has diverged to ~1e10, so only the
+        # sign and the first digits are comparable
+        assert tr[i, 0, 9] < 0 and r["trace"][0, 9] < 0
+        assert abs(tr[i, 0, 9] - r["trace"][0, 9]) <= 5e-2 * abs(r["trace"][0, 9])
     log_parity("solve/ascent_crocoddyl", B=B, neg_accepted=sum(r["neg_accepted"] for r in ref))
 
 
-def test_trace_matches_oracle():
+@pytest.mark.parametrize("regime,tol", [("tracking", 1e-9), ("random", 2e-7)])
+def test_trace_matches_oracle(regime, tol):
     """ffddp_trace_*: the per-iteration record CallbackVerbose prints (iter,
     cost, stop, grad, preg, dreg, step, ffeas, dV, dV_exp) equals the
-    oracle's, iteration by iteration; iterations not run are NaN rows."""
+    oracle's, iteration by iteration; iterations not run are NaN rows.
+    Tolerances: the regime's full-solve tolerance (random x0: 2e-7, as
+    test_solve_random_regime_horizon30)."""
     N, B, it = 30, 4, 12
     cfg = product_cfg("classical", N)
-    b = make_batch("classical", B, N, seed=23, surface=1, regime="random")
+    b = make_batch("classical", B, N, seed=23, surface=1, regime=regime)
     solver = BatchedBoxFDDP(cfg, max_batch=B)
     solver.trace_enable(it)
     solver.solve(b, maxiter=10, is_feasible=False)
@@ -254,10 +262,12 @@ def test_trace_matches_oracle():
         for col in (0, 4, 5, 6):  # iter, preg, dreg, step: exact
             assert np.array_equal(g[:, col], o[:, col]), (i, _abi.TRACE_FIELDS[col])
         for col in (1, 2, 3, 7, 8, 9):
-            e = float(np.max(np.abs(g[:, col] - o[:, col]) / np.maximum(1.0, np.abs(o[:, col]))))
+            # dV, dV_exp: differences of costs, relative to the cost
+            scale = np.abs(o[:, 1]) if col >= 8 else np.abs(o[:, col])
+            e = float(np.max(np.abs(g[:, col] - o[:, col]) / np.maximum(1.0, scale)))
             worst = max(worst, e)
-            assert e < 1e-8, (i, _abi.TRACE_FIELDS[col], e)
-    log_parity("trace/classical/random", B=B, worst=worst)
+            assert e < tol, (i, _abi.TRACE_FIELDS[col], e)
+    log_parity(f"trace/classical/{regime}", B=B, worst=worst)
     # the CallbackVerbose replay of instance 0
     from ffddp.callbacks import CallbackVerbose
     import io

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-2 GPU recipe: GPU tests, kernel-trace stats of the timed configuration
+# GPU profile recipe: GPU tests, kernel-trace stats of the timed configuration
 # (4 slices) and of the single-stream profiling step, FETCH_SIZE / WRITE_SIZE
 # in separate --pmc passes, then the full default bench line.
-# usage: tools/gpu_r02.sh TAG [skip-tests]
+# usage: tools/gpu_prof.sh TAG [skip-tests]
 set -e
 R=${GRAFT_REPO_ROOT:-/root/repo}
-TAG=${1:-r02}
+TAG=${1:-prof}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
