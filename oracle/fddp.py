@@ -52,6 +52,12 @@ class Consts:
     qp_th_acceptstep: float = 0.1
     qp_th_grad: float = 1e-5
     qp_reg: float = 0.0
+    # feasible-iteration gains on the BoxQP free set: "crocoddyl" = K =
+    # Quu_inv Qxu^T with the explicit Hff_inv (SolverBoxFDDP::computeGains),
+    # "solve" = Cholesky solves with Hff's factor, the HIP kernel's evaluation
+    # order.  Same mathematics; the explicit inverse carries ~100x more
+    # rounding error (tools/ext_budget.py, profiles/r03_ext_budget.jsonl).
+    gains_form: str = "crocoddyl"
 
 
 class BackwardError(Exception):
@@ -75,15 +81,16 @@ def llt(H):
         d = H[j, j] - np.dot(L[j, :j], L[j, :j])
         if not (d > 0.0):
             raise BackwardError("llt")
-        L[j, j] = math.sqrt(d)
+        L[j, j] = np.sqrt(d)
         for i in range(j + 1, n):
             L[i, j] = (H[i, j] - np.dot(L[i, :j], L[j, :j])) / L[j, j]
     return L
 
 
 def llt_solve(L, B):
-    Y = np.linalg.solve(L, B)
-    return np.linalg.solve(L.T, Y)
+    Y = ocp.solve(L, B if B.ndim == 2 else B[:, None])
+    X = ocp.solve(L.T, Y)
+    return X if B.ndim == 2 else X[:, 0]
 
 
 def boxqp(H, q, lb, ub, xinit, c: Consts):
@@ -104,13 +111,13 @@ def boxqp(H, q, lb, ub, xinit, c: Consts):
         if c.qp_reg != 0.0:
             Hff[np.diag_indices(nf)] += c.qp_reg
         L = llt(Hff) if nf > 0 else np.zeros((0, 0))
-        Hff_inv = llt_solve(L, np.eye(nf)) if nf > 0 else np.zeros((0, 0))
+        Hff_inv = llt_solve(L, np.eye(nf, dtype=H.dtype)) if nf > 0 else np.zeros((0, 0))
         dxf = -q[free]
         if clamped:
             dxf = dxf - H[np.ix_(free, clamped)] @ x[clamped]
         dxf = llt_solve(L, dxf) if nf > 0 else dxf
         dxf = dxf - x[free]
-        dx = np.zeros(n)
+        dx = np.zeros(n, dtype=np.result_type(H, q))
         dx[free] = dxf
         if np.max(np.abs(dx)) < c.qp_th_grad:
             break
@@ -158,9 +165,13 @@ class Stats:
 class SolverBoxFDDP:
     """Per-instance solver on one ocp.Problem (setProblem + solve surface)."""
 
-    def __init__(self, cfg_or_model, prob: ocp.Problem | None = None, box: bool = True, consts: Consts | None = None):
+    def __init__(self, cfg_or_model, prob: ocp.Problem | None = None, box: bool = True, consts: Consts | None = None,
+                 dtype=np.float64):
         """SolverBoxFDDP(problem): either (OCPConfig, Problem) for the reference
-        OCP, or a model object with running()/terminal()/x0/N/nx/nu/u_lb/u_ub."""
+        OCP, or a model object with running()/terminal()/x0/N/nx/nu/u_lb/u_ub.
+        dtype: the solver's working precision (np.longdouble for the
+        extended-precision error budget, tools/ext_budget.py); fp64 results
+        are unchanged by it."""
         model = ocp.RobotOCP(cfg_or_model, prob) if prob is not None else cfg_or_model
         self.model, self.box = model, box
         self.cfg, self.prob = getattr(model, "cfg", None), getattr(model, "prob", None)
@@ -168,12 +179,17 @@ class SolverBoxFDDP:
         self.th_stop = self.c.th_stop_box if box else self.c.th_stop_fddp
         N, nx, nu = model.N, model.nx, model.nu
         self.N, self.nx, self.nu = N, nx, nu
-        self.x0 = np.asarray(model.x0, float)
+        self.dt = np.dtype(dtype)
+        self.x0 = np.asarray(model.x0, self.dt)
         self.u_lb = np.asarray(model.u_lb, float)
         self.u_ub = np.asarray(model.u_ub, float)
-        self.k = np.zeros((N, nu))
-        self.K = np.zeros((N, nu, nx))
+        self.k = np.zeros((N, nu), self.dt)
+        self.K = np.zeros((N, nu, nx), self.dt)
         self.stats = Stats()
+
+    def _num(self, v):
+        """A scalar in the working precision (a Python float for fp64)."""
+        return float(v) if self.dt == np.float64 else self.dt.type(v)
 
     # --- problem evaluations -------------------------------------------------
     def _calc_diff(self):
@@ -181,12 +197,12 @@ class SolverBoxFDDP:
         run = self.model.running(slice(0, N), self.xs[:N], self.us, True)
         term = self.model.terminal(self.xs[N], True)
         self.run, self.term = run, term
-        self.cost = float(np.sum(run["cost"]) + term["cost"])  # ShootingProblem::calcDiff sum
-        self.fs = np.zeros((N + 1, self.nx))
+        self.cost = self._num(np.sum(run["cost"]) + term["cost"])  # ShootingProblem::calcDiff sum
+        self.fs = np.zeros((N + 1, self.nx), self.dt)
         if not self.is_feasible:
             self.fs[0] = self.x0 - self.xs[0]
             self.fs[1:] = run["xnext"] - self.xs[1:]
-        self.ffeas = float(np.max(np.abs(self.fs)))  # ||ffeas||_inf of this calcDiff
+        self.ffeas = self._num(np.max(np.abs(self.fs)))  # ||ffeas||_inf of this calcDiff
 
     def _backward(self):
         N, c = self.N, self.c
@@ -194,8 +210,8 @@ class SolverBoxFDDP:
         preg = self.preg
         Vxx = [None] * (N + 1)
         Vx = [None] * (N + 1)
-        Qu = np.zeros((N, self.nu))
-        Quu = np.zeros((N, self.nu, self.nu))
+        Qu = np.zeros((N, self.nu), self.dt)
+        Quu = np.zeros((N, self.nu, self.nu), self.dt)
         K = self.K  # Crocoddyl overwrites K_/k_ in place (a retried pass sees partial updates)
         k = self.k
         Vxx[N] = term["Lxx"].copy() + preg * np.eye(self.nx)
@@ -221,10 +237,14 @@ class SolverBoxFDDP:
                 lb = self.u_lb - self.us[t]
                 ub = self.u_ub - self.us[t]
                 x, free, clamped, Hff_inv = boxqp(Quu_t, Qu_t, lb, ub, self.k[t], c)
-                Quu_inv = np.zeros((self.nu, self.nu))
+                Quu_inv = np.zeros((self.nu, self.nu), self.dt)
                 if free:
                     Quu_inv[np.ix_(free, free)] = Hff_inv
-                K[t] = Quu_inv @ Qxu.T
+                if c.gains_form == "crocoddyl" or not free:
+                    K[t] = Quu_inv @ Qxu.T
+                else:  # "solve": K_f = Hff^-1 Qxu_f^T by the Cholesky factor (the HIP kernel's order)
+                    K[t] = 0.0
+                    K[t][free] = llt_solve(llt(Quu_t[np.ix_(free, free)]), Qxu.T[free])
                 k[t] = -x
                 if clamped:
                     self.stats.clamped += 1
@@ -268,7 +288,7 @@ class SolverBoxFDDP:
         N = self.N
         xs_try = np.zeros_like(self.xs)
         us_try = np.zeros_like(self.us)
-        cost_try = 0.0
+        cost_try = self._num(0.0)
         xnext = self.x0.copy()
         gap = not (self.is_feasible or alpha == 1.0)
         for t in range(N):
@@ -280,13 +300,13 @@ class SolverBoxFDDP:
             us_try[t] = u
             d = self.model.running(t, xs_try[t], us_try[t], False)
             xnext = d["xnext"]
-            cost_try += float(d["cost"])
-            if raise_if_nan(cost_try) or raise_if_nan(float(np.max(np.abs(xnext)))):
+            cost_try += self._num(d["cost"])
+            if raise_if_nan(float(cost_try)) or raise_if_nan(float(np.max(np.abs(xnext)))):
                 raise ForwardError("nan")
         xs_try[N] = xnext + self.fs[N] * (alpha - 1.0) if gap else xnext
         d = self.model.terminal(xs_try[N], False)
-        cost_try += float(d["cost"])
-        if raise_if_nan(cost_try):
+        cost_try += self._num(d["cost"])
+        if raise_if_nan(float(cost_try)):
             raise ForwardError("nan")
         return xs_try, us_try, cost_try
 
@@ -299,13 +319,13 @@ class SolverBoxFDDP:
     # --- SolverFDDP::solve -----------------------------------------------------
     def solve(self, xs_init, us_init, maxiter: int = 10, is_feasible: bool = False, init_reg: float = float("nan")):
         c = self.c
-        self.xs = np.array(xs_init, dtype=float, copy=True)
-        self.us = np.array(us_init, dtype=float, copy=True)
+        self.xs = np.array(xs_init, dtype=self.dt, copy=True)
+        self.us = np.array(us_init, dtype=self.dt, copy=True)
         self.is_feasible = bool(is_feasible)
         self.preg = c.reg_min if math.isnan(init_reg) else float(init_reg)
         self.was_feasible = False
-        self.k = np.zeros((self.N, self.nu))
-        self.K = np.zeros((self.N, self.nu, self.nx))
+        self.k = np.zeros((self.N, self.nu), self.dt)
+        self.K = np.zeros((self.N, self.nu, self.nx), self.dt)
         self.stats = Stats()
         self.stop = float("nan")
         # CallbackVerbose records (include/ffddp.h ffddp_trace_*): iter, cost,
@@ -362,7 +382,7 @@ class SolverBoxFDDP:
                 self._increase_reg()
                 if self.preg == c.reg_max:
                     return False
-            self.stop = float(np.sum(self.Qu * self.Qu))
+            self.stop = self._num(np.sum(self.Qu * self.Qu))
             self.trace.append((it, self.cost, self.stop, -td1, self.preg, self.preg, steplength, self.ffeas, tdV, tdVexp))
             if self.was_feasible and self.stop < self.th_stop:
                 return True

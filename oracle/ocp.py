@@ -146,6 +146,89 @@ class Problem:
 
 
 # ---------------------------------------------------------------------------
+# dense solves: LAPACK for fp64 (and complex128), else (np.longdouble, the
+# extended-precision error-budget runs, tools/ext_budget.py) Gaussian
+# elimination with partial pivoting in the array's own precision
+# ---------------------------------------------------------------------------
+_LAPACK = (np.dtype(np.float64), np.dtype(np.complex128))
+
+
+def solve(A, b):
+    """np.linalg.solve(A, b) for batched A (..., n, n), b (..., n, k)."""
+    if A.dtype in _LAPACK and b.dtype in _LAPACK:
+        return np.linalg.solve(A, b)
+    dt = np.result_type(A, b)
+    A = np.array(A, dtype=dt, copy=True)
+    X = np.array(np.broadcast_to(b, A.shape[:-2] + b.shape[-2:]), dtype=dt, copy=True)
+    n = A.shape[-1]
+    for j in range(n):
+        piv = j + np.argmax(np.abs(A[..., j:, j]), axis=-1)  # (...)
+        idx = np.indices(piv.shape)
+        rows_j = A[..., j, :].copy()
+        A[..., j, :] = A[(*idx, piv)]
+        A[(*idx, piv)] = rows_j
+        xj = X[..., j, :].copy()
+        X[..., j, :] = X[(*idx, piv)]
+        X[(*idx, piv)] = xj
+        for i in range(j + 1, n):
+            f = A[..., i, j] / A[..., j, j]
+            A[..., i, :] = A[..., i, :] - f[..., None] * A[..., j, :]
+            X[..., i, :] = X[..., i, :] - f[..., None] * X[..., j, :]
+    for j in range(n - 1, -1, -1):
+        acc = X[..., j, :]
+        for m in range(j + 1, n):
+            acc = acc - A[..., j, m][..., None] * X[..., m, :]
+        X[..., j, :] = acc / A[..., j, j][..., None]
+    return X
+
+
+def inv(A):
+    if A.dtype in _LAPACK:
+        return np.linalg.inv(A)
+    return solve(A, np.broadcast_to(np.eye(A.shape[-1], dtype=A.dtype), A.shape))
+
+
+def cholesky(A):
+    """Lower Cholesky factor of batched SPD A (..., n, n), any float dtype."""
+    n = A.shape[-1]
+    L = np.zeros_like(A)
+    for j in range(n):
+        d = A[..., j, j] - np.sum(L[..., j, :j] * L[..., j, :j], -1)
+        L[..., j, j] = np.sqrt(d)
+        for i in range(j + 1, n):
+            L[..., i, j] = (A[..., i, j] - np.sum(L[..., i, :j] * L[..., j, :j], -1)) / L[..., j, j]
+    return L
+
+
+def tri_lower_solve(L, B):
+    """L^-1 B (forward substitution), L (..., n, n) lower, B (..., n, k)."""
+    n = L.shape[-1]
+    X = np.array(np.broadcast_to(B, L.shape[:-2] + B.shape[-2:]), dtype=np.result_type(L, B), copy=True)
+    for i in range(n):
+        acc = X[..., i, :]
+        for m in range(i):
+            acc = acc - L[..., i, m][..., None] * X[..., m, :]
+        X[..., i, :] = acc / L[..., i, i][..., None]
+    return X
+
+
+def tri_upper_solve(L, B):
+    """L^-T B (back substitution with the transpose of lower L)."""
+    n = L.shape[-1]
+    X = np.array(np.broadcast_to(B, L.shape[:-2] + B.shape[-2:]), dtype=np.result_type(L, B), copy=True)
+    for i in range(n - 1, -1, -1):
+        acc = X[..., i, :]
+        for m in range(i + 1, n):
+            acc = acc - L[..., m, i][..., None] * X[..., m, :]
+        X[..., i, :] = acc / L[..., i, i][..., None]
+    return X
+
+
+def chol_solve(L, B):
+    return tri_upper_solve(L, tri_lower_solve(L, B))
+
+
+# ---------------------------------------------------------------------------
 # activations (crocoddyl ActivationModel{Quad,WeightedQuad,QuadraticBarrier})
 # ---------------------------------------------------------------------------
 def act_quad(r):
@@ -224,32 +307,39 @@ def contact_star(cfg, p_ref):
 
 
 def dynamics(cfg, q, v, tau, surface, p_star):
-    """Forward dynamics.  Returns a, lam (or None), and the KKT pieces."""
+    """Forward dynamics.  Free: a = M^-1 (tau - b).  Contact: the KKT system
+    [[M, Jc^T], [Jc, -eps I]] [a; -lam] = [tau - b; -gamma], solved as
+    pinocchio::forwardDynamics(model, data, q, v, tau, J, gamma, inv_damping)
+    does it (Crocoddyl's ContactFwdDynamics calc): Cholesky of M, Y = L^-1
+    Jc^T, S = Jc M^-1 Jc^T + eps I = Y^T Y + eps I, lam = -S^-1 (Jc M^-1
+    (tau - b) + gamma), a = M^-1 (tau - b + Jc^T lam).  (A dense LU of the
+    eps = 1e-8 KKT matrix loses ~8 digits: tools/ext_budget.py.)"""
     M = P.crba(q)
     b = P.rnea(q, v, np.zeros_like(q))
+    L = cholesky(M)
+    r = (tau - b)[..., None]
+    Mr = chol_solve(L, r)  # M^-1 (tau - b)
     if not surface:
-        a = np.linalg.solve(M, (tau - b)[..., None])[..., 0]
-        return dict(a=a, lam=None, M=M)
+        return dict(a=Mr[..., 0], lam=None, M=M, L=L)
     Jc, gam = _contact_terms(cfg, q, v, np.zeros_like(q), p_star)
     nc = cfg.nc
-    K = np.zeros(q.shape[:-1] + (7 + nc, 7 + nc))
-    K[..., :7, :7] = M
-    K[..., :7, 7:] = np.swapaxes(Jc, -1, -2)
-    K[..., 7:, :7] = Jc
-    K[..., 7:, 7:] = -cfg.contact_inv_damping * np.eye(nc)
-    rhs = np.concatenate([tau - b, -gam], -1)
-    y = np.linalg.solve(K, rhs[..., None])[..., 0]
-    return dict(a=y[..., :7], lam=-y[..., 7:], M=M, K=K)
+    Y = tri_lower_solve(L, np.swapaxes(Jc, -1, -2))  # (..., 7, nc)
+    S = P.mm(np.swapaxes(Y, -1, -2), Y) + cfg.contact_inv_damping * np.eye(nc)
+    Ls = cholesky(S)
+    lam = -chol_solve(Ls, P.mm(Jc, Mr) + gam[..., None])  # (..., nc, 1)
+    a = Mr + chol_solve(L, P.mm(np.swapaxes(Jc, -1, -2), lam))
+    return dict(a=a[..., 0], lam=lam[..., 0], M=M, L=L, Jc=Jc, Ls=Ls)
 
 
 def dynamics_derivatives(cfg, q, v, dyn, surface, p_star):
     """Fx (…,7,14), Fu (…,7,7), df_dx (…,nc,14), df_du (…,nc,7)."""
     a = dyn["a"]
     x = np.concatenate([q, v], -1)
+    eye7 = np.broadcast_to(np.eye(7, dtype=dyn["L"].dtype), dyn["L"].shape)
+    Minv = chol_solve(dyn["L"], eye7)
     if not surface:
         tau_fn = lambda X: P.rnea(X[..., :7], X[..., 7:], a.astype(X.dtype))
         dtau = P.complex_step_jacobian(tau_fn, x)
-        Minv = np.linalg.inv(dyn["M"])
         return dict(Fx=-P.mm(Minv, dtau), Fu=Minv, dfdx=None, dfdu=None)
     lam = dyn["lam"]
     fvec = _force_vec(cfg, lam)
@@ -257,9 +347,16 @@ def dynamics_derivatives(cfg, q, v, dyn, surface, p_star):
     dtau = P.complex_step_jacobian(tau_fn, x)
     a0_fn = lambda X: _contact_terms(cfg, X[..., :7], X[..., 7:], a.astype(X.dtype), p_star)[1]
     da0 = P.complex_step_jacobian(a0_fn, x)
-    Kinv = np.linalg.inv(dyn["K"])
-    Kaa, Kal = Kinv[..., :7, :7], Kinv[..., :7, 7:]
-    Kla, Kll = Kinv[..., 7:, :7], Kinv[..., 7:, 7:]
+    # KKT inverse in the block form of pinocchio::getKKTContactDynamicMatrixInverse:
+    # [[Minv - Minv Jc^T S^-1 Jc Minv, Minv Jc^T S^-1], [S^-1 Jc Minv, -S^-1]]
+    Jc, Ls = dyn["Jc"], dyn["Ls"]
+    nc = Jc.shape[-2]
+    Sinv = chol_solve(Ls, np.broadcast_to(np.eye(nc, dtype=Ls.dtype), Ls.shape))
+    MJt = P.mm(Minv, np.swapaxes(Jc, -1, -2))  # (..., 7, nc)
+    Kal = P.mm(MJt, Sinv)
+    Kla = np.swapaxes(Kal, -1, -2)
+    Kaa = Minv - P.mm(Kal, np.swapaxes(MJt, -1, -2))
+    Kll = -Sinv
     Fx = -P.mm(Kaa, dtau) - P.mm(Kal, da0)
     dfdx = P.mm(Kla, dtau) + P.mm(Kll, da0)
     return dict(Fx=Fx, Fu=Kaa, dfdx=dfdx, dfdu=-Kla)
@@ -487,7 +584,7 @@ def iam_eval(cfg, refs, x, u, surface, mode, diff):
     if diff:
         Fa_x, Fa_u = d["Fx"], d["Fu"]
         batch = x.shape[:-1]
-        Fx = np.broadcast_to(np.eye(14), batch + (14, 14)).copy()
+        Fx = np.broadcast_to(np.eye(14, dtype=np.result_type(x, Fa_x)), batch + (14, 14)).copy()
         Fx[..., :7, :] += dt * dt * Fa_x
         Fx[..., 7:, :] += dt * Fa_x
         Fx[..., :7, 7:] += dt * np.eye(7)
@@ -533,14 +630,15 @@ def ff_augment(cfg, inner, y, w, yref, diff):
     out["cost"] = cost
     if diff:
         batch = y.shape[:-1]
-        Fx = np.zeros(batch + (21, 21))
+        fdt = np.result_type(y, inner["Fx"])
+        Fx = np.zeros(batch + (21, 21), dtype=fdt)
         Fx[..., :14, :14] = inner["Fx"]
         Fx[..., :14, 14:] = inner["Fu"]
         Fx[..., 14:, 14:] = alpha * np.eye(7)
-        Fu = np.zeros(batch + (21, 7))
+        Fu = np.zeros(batch + (21, 7), dtype=fdt)
         Fu[..., 14:, :] = beta * np.eye(7)
         Lx = np.concatenate([inner["Lx"], inner["Lu"]], -1)
-        Lxx = np.zeros(batch + (21, 21))
+        Lxx = np.zeros(batch + (21, 21), dtype=fdt)
         Lxx[..., :14, :14] = inner["Lxx"]
         Lxx[..., :14, 14:] = inner["Lxu"]
         Lxx[..., 14:, :14] = np.swapaxes(inner["Lxu"], -1, -2)

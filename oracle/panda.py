@@ -337,7 +337,7 @@ def complex_step_jacobian(f, x, h=1e-30):
     """d f / d x by complex step.  f maps (...,n)->(...,m); returns (...,m,n)."""
     n = x.shape[-1]
     E = np.eye(n)
-    X = x[None, ...].astype(complex) + 1j * h * E.reshape((n,) + (1,) * (x.ndim - 1) + (n,))
+    X = x[None, ...].astype(np.result_type(x.dtype, np.complex128)) + 1j * h * E.reshape((n,) + (1,) * (x.ndim - 1) + (n,))
     F = f(X)
     J = np.imag(F) / h  # (n, ..., m)
     return np.moveaxis(J, 0, -1)

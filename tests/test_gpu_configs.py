@@ -90,7 +90,11 @@ def test_c5_per_gpu_shape_point3d_n100(monkeypatch):
                 a, b = getattr(big, name)[i], getattr(small, name)[j]
                 assert np.array_equal(a, b, equal_nan=True), (name, int(i))
     sel = picks[::2]
-    ref = solve_many(cfg, batch, sel)
+    from oracle import fddp
+
+    # the solve-form oracle (K by Cholesky solves, the kernel's order): the
+    # budget's N = 100 figure is ~1e-10 (tests/test_gpu_parity.py CASE_TOL)
+    ref = solve_many(cfg, batch, sel, consts=fddp.Consts(gains_form="solve"))
     e = dict(xs=0.0, us=0.0, K=0.0, cost=0.0)
     for i, r in zip(sel, ref):
         assert bool(big.ok[i]) == r["ok"] and int(big.iter[i]) == r["iter"]
@@ -98,8 +102,7 @@ def test_c5_per_gpu_shape_point3d_n100(monkeypatch):
         for k in ("xs", "us", "K"):
             e[k] = max(e[k], rel_err(getattr(big, k)[i], r[k]))
         e["cost"] = max(e["cost"], rel_err(big.cost[i], r["cost"]))
-    log_parity(f"batch/point3d/N{N}/B{B}", n=len(sel), **e)
-    # point3d / N = 100 error budget: tests/test_gpu_parity.py CASE_TOL
-    assert max(e["xs"], e["us"], e["cost"]) < 6e-7 and e["K"] < 2e-6, e
+    log_parity(f"batch/point3d/N{N}/B{B}/solve_form", n=len(sel), **e)
+    assert max(e["xs"], e["us"], e["cost"]) < 1e-9 and e["K"] < 1e-9, e
     big.close()
     small.close()

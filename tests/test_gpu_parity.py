@@ -28,20 +28,38 @@ from oracle_pool import solve_many
 
 pytestmark = pytest.mark.gpu
 
-# observed maxima (profiles/r02_parity_errors.jsonl): calcDiff blocks <= 9e-14;
-# well-conditioned solves (normal_1d, FF, plain FDDP, clamped, retries)
-# xs/us/cost <= 4e-11, K <= 3e-11.  Contact point3d goes through the 3x3
-# KKT Schur complement with 1e-8 damping (oracle: dense KKT solve), which
-# amplifies rounding differences; those cases carry their own tolerances.
+# observed maxima (profiles/r02_parity_errors.jsonl, r03): calcDiff blocks
+# <= 9e-14; well-conditioned solves (normal_1d, FF, plain FDDP, clamped,
+# retries) xs/us/cost <= 4e-11, K <= 3e-11.
 TOL_NODE = 1e-12
 TOL_SOLVE = 1e-10
 TOL_K = 3e-10
-# case -> (xs/us/cost tolerance, K tolerance), ~10x the observed maxima
+# Error budget (tools/ext_budget.py -> profiles/r03_ext_budget.jsonl: each
+# fp64 implementation against an x87 extended-precision solve of the same
+# inputs).  The HIP library is within ~2e-9 of the extended answer in every
+# case.  The oracle's default gains form -- K = Hff_inv Qxu^T with the
+# explicit BoxQP inverse, as SolverBoxFDDP::computeGains writes it -- carries
+# up to 1e-7 (point3d + friction cone) / 2.3e-7 (K at N = 100) of rounding
+# error itself; with K by Cholesky solves (Consts.gains_form = "solve", the
+# kernel's order, same mathematics) the oracle is back within ~3e-9.  So
+# the tight tolerances below hold against the solve form; the explicit-inverse
+# form is checked at budget tolerances (CROCODDYL_FORM_TOL).
+# case -> (xs/us/cost tolerance, K tolerance) vs the solve-form oracle,
+# ~10x the observed maxima.  classical point3d + friction cone: every fp64
+# implementation sits 1-3e-9 from the extended answer (the cone's barrier
+# Hessian makes this problem the least well conditioned), so 1e-8 / 5e-9.
 CASE_TOL = {
-    ("classical", "point3d", 1, 0): (6e-9, 7e-8),
-    ("classical", "point3d", 1, 1): (1e-6, 1.2e-7),
-    ("ff", "point3d", 1, 1): (2e-8, 3e-8),
+    ("classical", "point3d", 1, 1): (1e-8, 5e-9),
+    ("ff", "point3d", 1, 1): (3e-9, 5e-9),
 }
+# vs the explicit-inverse (Crocoddyl-order) oracle: its own rounding error
+CROCODDYL_FORM_TOL = {
+    ("classical", "point3d", 1, 0): (6e-9, 3e-8),
+    ("classical", "point3d", 1, 1): (1e-6, 1.5e-7),
+    ("ff", "point3d", 1, 0): (TOL_SOLVE, TOL_K),
+    ("ff", "point3d", 1, 1): (3e-8, 3e-8),
+}
+SOLVE_FORM = fddp.Consts(gains_form="solve")
 
 CASES = [
     ("classical", "normal_1d", 1, 0),
@@ -120,9 +138,18 @@ def test_solve_matches_oracle(variant, contact, surf, cone):
     b = make_batch(variant, B, N, seed=21 + surf, surface=surf)
     solver = BatchedBoxFDDP(cfg, max_batch=B)
     solver.solve(b, maxiter=10, is_feasible=False)
+    key = (variant, contact, surf, cone)
+    name = f"solve/{variant}/{contact}/surf{surf}/cone{cone}"
+    if key in CROCODDYL_FORM_TOL:
+        ref = solve_many(cfg, b, range(B), consts=SOLVE_FORM)
+        tol, tol_k = CASE_TOL.get(key, (TOL_SOLVE, TOL_K))
+        _check_solves(name + "/solve_form", cfg, b, solver, ref, tol, tol_k)
+        tol, tol_k = CROCODDYL_FORM_TOL[key]
+        name += "/crocoddyl_form"
+    else:
+        tol, tol_k = TOL_SOLVE, TOL_K
     ref = solve_many(cfg, b, range(B))
-    tol, tol_k = CASE_TOL.get((variant, contact, surf, cone), (TOL_SOLVE, TOL_K))
-    _check_solves(f"solve/{variant}/{contact}/surf{surf}/cone{cone}", cfg, b, solver, ref, tol, tol_k)
+    _check_solves(name, cfg, b, solver, ref, tol, tol_k)
 
 
 def test_solve_random_regime_horizon30():
@@ -134,6 +161,10 @@ def test_solve_random_regime_horizon30():
     solver = BatchedBoxFDDP(cfg, max_batch=B)
     solver.solve(b, maxiter=10, is_feasible=False)
     ref = solve_many(cfg, b, range(B))
+    # unconverged 10-iteration solves from far-off starts: every fp64
+    # implementation (this library, the oracle in both gains forms, the C++
+    # baseline) is 1e-9..8e-9 from the extended-precision answer on the first
+    # 8 instances (profiles/r03_ext_budget.jsonl); observed here 1.7e-8
     _check_solves("solve/random/N30/B32", cfg, b, solver, ref, tol=2e-7, tol_k=4e-8)
 
 
@@ -266,7 +297,9 @@ def test_trace_matches_oracle(regime, tol):
             scale = np.abs(o[:, 1]) if col >= 8 else np.abs(o[:, col])
             e = float(np.max(np.abs(g[:, col] - o[:, col]) / np.maximum(1.0, scale)))
             worst = max(worst, e)
-            assert e < tol, (i, _abi.TRACE_FIELDS[col], e)
+            # stop = sum ||Qu||^2: a squared gradient, its error is
+            # ~ |Qu| |Quu| |dx| (random x0: 3.3e-7 observed at the 2e-8 level of xs / us)
+            assert e < (20 * tol if col == 2 else tol), (i, _abi.TRACE_FIELDS[col], e)
     log_parity(f"trace/classical/{regime}", B=B, worst=worst)
     # the CallbackVerbose replay of instance 0
     from ffddp.callbacks import CallbackVerbose
@@ -306,8 +339,12 @@ def test_long_horizon_point3d_matches_oracle():
     b = make_batch("classical", B, N, seed=55, surface=1)
     solver = BatchedBoxFDDP(cfg, max_batch=B)
     solver.solve(b, maxiter=10, is_feasible=False)
+    # solve-form oracle: observed 1.7e-11 / 6.2e-11 / K 7.2e-11 (r03 budget)
+    ref = solve_many(cfg, b, range(B), consts=SOLVE_FORM)
+    _check_solves("solve/point3d/N100/solve_form", cfg, b, solver, ref, tol=TOL_SOLVE, tol_k=TOL_K)
+    # explicit-inverse oracle: its own error is 2.3e-8 / 6.3e-8 / K 2.3e-7
     ref = solve_many(cfg, b, range(B))
-    _check_solves("solve/point3d/N100", cfg, b, solver, ref, tol=6e-7, tol_k=2e-6)
+    _check_solves("solve/point3d/N100/crocoddyl_form", cfg, b, solver, ref, tol=6e-7, tol_k=2e-6)
 
 
 def test_gravity_torque_dev_matches_oracle():
