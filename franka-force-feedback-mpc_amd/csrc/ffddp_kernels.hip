@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -1647,6 +1648,10 @@ struct ffddp_handle {
 
 namespace {
 
+bool stream_pool_acquire(int device, int n, std::vector<hipStream_t>& out);
+void stream_pool_release(int device, int n);
+
+
 int fail(ffddp_handle* h, int code, const std::string& msg) {
   if (h) h->err = msg;
   return code;
@@ -1738,11 +1743,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
   int S = h->nstreams;
   if (B < 64 * S) S = 1;
   if (S > 1 && (int)h->streams.size() < S) {
-    while ((int)h->streams.size() < S) {
-      hipStream_t st;
-      HIPCHK(h, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-      h->streams.push_back(st);
-    }
+    if (!stream_pool_acquire(h->device, S, h->streams)) return fail(h, FFDDP_E_DEVICE, "hipStreamCreate failed");
     while ((int)h->sev.size() < S + 1) {
       hipEvent_t e;
       HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1921,6 +1922,45 @@ void launch_node(ffddp_handle* h, Dev d, int B, hipStream_t s, int force_all) {
   const long nodes = (long)B * (h->hc.N + 1);
   hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, s, h->dc,
                      d, h->in_x0, h->in_nref, h->in_iref, h->in_surf, force_all, 0);
+}
+
+// Slice streams shared by every handle of the process on a device: a
+// process gets 4 hardware queues (GPU_MAX_HW_QUEUES), and every stream
+// beyond them shares a queue with another, serialising two slices (a second
+// handle's own 3 streams took a B = 4096 host-entry solve from 11.4 to
+// 15.4 ms).  Handles are not thread-safe anyway; two handles used from one
+// thread just queue their slices on the same streams.  Ref-counted: the last
+// release destroys them.
+struct StreamPool {
+  std::vector<hipStream_t> s;
+  int refs = 0;
+};
+std::mutex g_pool_mu;
+StreamPool g_pool[64];
+
+bool stream_pool_acquire(int device, int n, std::vector<hipStream_t>& out) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  StreamPool& p = g_pool[device & 63];
+  while ((int)p.s.size() < n) {
+    hipStream_t st;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+    p.s.push_back(st);
+  }
+  const int had = (int)out.size();
+  out.assign(p.s.begin(), p.s.begin() + n);
+  p.refs += n - had;
+  return true;
+}
+
+void stream_pool_release(int device, int n) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  StreamPool& p = g_pool[device & 63];
+  p.refs -= n;
+  if (p.refs <= 0) {
+    for (hipStream_t st : p.s) (void)hipStreamDestroy(st);
+    p.s.clear();
+    p.refs = 0;
+  }
 }
 
 // page-locked (hipHostMalloc'd / registered) host memory?
@@ -2115,7 +2155,7 @@ void ffddp_destroy(ffddp_handle* h) {
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->sev) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->stg) (void)hipEventDestroy(e);
-  for (hipStream_t st : h->streams) (void)hipStreamDestroy(st);
+  if (!h->streams.empty()) stream_pool_release(h->device, (int)h->streams.size());
   for (hipEvent_t e : h->hdone) (void)hipEventDestroy(e);
   free_all(h);
   delete h;

@@ -293,8 +293,8 @@ def test_trace_matches_oracle(regime, tol):
         for col in (0, 4, 5, 6):  # iter, preg, dreg, step: exact
             assert np.array_equal(g[:, col], o[:, col]), (i, _abi.TRACE_FIELDS[col])
         for col in (1, 2, 3, 7, 8, 9):
-            # dV, dV_exp: differences of costs, relative to the cost
-            scale = np.abs(o[:, 1]) if col >= 8 else np.abs(o[:, col])
+            # grad = -d1, dV, dV_exp: cost changes, relative to the cost
+            scale = np.abs(o[:, 1]) if col in (3, 8, 9) else np.abs(o[:, col])
             e = float(np.max(np.abs(g[:, col] - o[:, col]) / np.maximum(1.0, scale)))
             worst = max(worst, e)
             # stop = sum ||Qu||^2: a squared gradient, its error is
