@@ -181,6 +181,47 @@ template <bool ROW = false> __device__ __forceinline__ double g8_solve(const dou
   return out;
 }
 
+// Per-lane (joint) constants of the group calc, staged once per block in LDS
+// (lane 7: the end-effector offset in R / p, zero inertia).  Read from the
+// constant struct with lane-indexed addresses they were vector-memory loads
+// inside the rollout's node loop, and since vmcnt counts loads and stores
+// together every such load also waited for the next node's prefetch and the
+// trial's stores.
+struct LaneK {
+  double R[9], p[3], com[3], I[9];
+  double m, vdw, qsx, qslb, qsub, tslb, tsub, ulb, uub, wy2q, wy2v, wy2t, wslim;
+};
+
+// lane li < 8 of the block fills LK[li]; the caller synchronises
+__device__ __forceinline__ void lane_consts_fill(const DevConsts& C, LaneK* LK, int li) {
+  if (li >= G8) return;
+  const ffddp_robot& rb = C.rb;
+  LaneK& k = LK[li];
+  const bool J = li < NQ;
+  const int j = J ? li : NQ - 1;
+  for (int e = 0; e < 9; ++e) {
+    k.R[e] = J ? rb.joint_R[j][e] : rb.ee_R[e];
+    k.I[e] = J ? rb.inertia[j][e] : 0.0;
+  }
+  for (int e = 0; e < 3; ++e) {
+    k.p[e] = J ? rb.joint_p[j][e] : rb.ee_p[e];
+    k.com[e] = J ? rb.com[j][e] : 0.0;
+  }
+  k.m = J ? rb.mass[j] : 0.0;
+  k.vdw = C.vdw[j];
+  k.qsx = C.qs_xref[j];
+  k.qslb = C.qs_lb[j];
+  k.qsub = C.qs_ub[j];
+  k.tslb = C.ts_lb[j];
+  k.tsub = C.ts_ub[j];
+  k.ulb = C.u_lb[j];
+  k.uub = C.u_ub[j];
+  k.wy2q = C.Wy2[j];
+  k.wy2v = C.Wy2[7 + j];
+  k.wy2t = C.Wy2[14 + j];
+  k.wslim = C.ws_lim[j];
+}
+
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* c) {
   c[0] = a[1] * b[2] - a[2] * b[1];
   c[1] = a[2] * b[0] - a[0] * b[2];
@@ -194,9 +235,9 @@ __device__ __forceinline__ void cross3(const double* a, const double* b, double*
 //   cpart (this lane's share of the unscaled DAM cost: g8_sum gives P.cost),
 //   lam (contact force, group-uniform; zero in free mode).
 template <int NC>
-__device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool surface, double q, double v, double u,
-                                             double xq, double xv, double tr, const double* ref, double& qn,
-                                             double& vn, double& cpart, double (&lam)[3]
+__device__ __forceinline__ void node_calc_g8(const DevConsts& C, const LaneK& K, int mode, bool surface, double q,
+                                             double v, double u, double xq, double xv, double tr, const double* ref,
+                                             double& qn, double& vn, double& cpart, double (&lam)[3]
 #ifdef FFDDP_PHASE_PROF
                                              , unsigned long long (&pp_acc)[12], unsigned long long& pp_last
 #endif
@@ -214,21 +255,19 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
   if (J) {
     double s, c;
     sincos_(q, s, c);
-    const double* Jr = rb.joint_R[ji];
+    const double* Jr = K.R;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       R[3 * r + 0] = c * Jr[3 * r + 0] + s * Jr[3 * r + 1];
       R[3 * r + 1] = c * Jr[3 * r + 1] - s * Jr[3 * r + 0];
       R[3 * r + 2] = Jr[3 * r + 2];
     }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) o[k] = rb.joint_p[ji][k];
   } else {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) R[k] = rb.ee_R[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) o[k] = rb.ee_p[k];
+    for (int k = 0; k < 9; ++k) R[k] = K.R[k];
   }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o[k] = K.p[k];
 #pragma unroll
   for (int d = 1; d < G8; d <<= 1) {
     double Rp[9], op[3];
@@ -359,11 +398,11 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
     if (C.variant == FFDDP_CLASSICAL || C.inner_state_reg) {
       const double rq = q - xq, rv = v - xv;
       cj += C.w_post * (0.5 * (rq * rq + rv * rv));
-      cj += C.w_v * (0.5 * (C.vdw[ji] * v * v));
+      cj += C.w_v * (0.5 * (K.vdw * v * v));
     }
     if (C.has_qsoft) {
       double ai, Ar, Arr;
-      barrier(q - C.qs_xref[ji], C.qs_lb[ji], C.qs_ub[ji], ai, Ar, Arr);
+      barrier(q - K.qsx, K.qslb, K.qsub, ai, Ar, Arr);
       cj += C.w_qs * ai;
     }
     if (!terminal && (C.variant == FFDDP_CLASSICAL || C.inner_tau_reg)) {
@@ -371,7 +410,7 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
       cj += C.w_tau * (0.5 * r * r);
       if (C.has_tsoft) {
         double ai, Ar, Arr;
-        barrier(u, C.ts_lb[ji], C.ts_ub[ji], ai, Ar, Arr);
+        barrier(u, K.tslb, K.tsub, ai, Ar, Arr);
         cj += C.w_ts * ai;
       }
     }
@@ -383,12 +422,12 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, int mode, bool 
     double fl[3] = {0, 0, 0}, fa[3] = {0, 0, 0};
     double tm = 0.0, th[3] = {0, 0, 0}, tI[6] = {0, 0, 0, 0, 0, 0};
     if (J) {
-      const double m = rb.mass[ji];
-      const double* Ic = rb.inertia[ji];
+      const double m = K.m;
+      const double* Ic = K.I;
       double cw[3];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
-        cw[r] = o[r] + (R[3 * r + 0] * rb.com[ji][0] + R[3 * r + 1] * rb.com[ji][1] + R[3 * r + 2] * rb.com[ji][2]);
+        cw[r] = o[r] + (R[3 * r + 0] * K.com[0] + R[3 * r + 1] * K.com[1] + R[3 * r + 2] * K.com[2]);
       // world inertia Iw = R Ic R^T
       double IcR[9], Iw[9];
 #pragma unroll

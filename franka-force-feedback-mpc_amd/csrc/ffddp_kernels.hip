@@ -1112,6 +1112,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
   const bool J = li < NQ;
   const int ji = J ? li : 0;
   const int slot = (int)(gid / ntr), tr = tr0 + (int)(gid % ntr);
+  __shared__ LaneK LKs[G8];
+  lane_consts_fill(C, LKs, (int)threadIdx.x);
+  __syncthreads();
+  const LaneK& K = LKs[li];
   const ActiveList al = active_list(d, cur);
   if (slot >= al.n) return;
   const int b = al.list[slot];
@@ -1134,8 +1138,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
   const bool gap = !(feas || alpha == 1.0);
   const bool surf = surface[b] != 0;
   const double* xreg = inst_ref + (long)b * 21;
-  const double* yref = x0 + (long)b * nx;
   const double xq = xreg[ji], xv = xreg[7 + ji], tref = xreg[14 + ji];
+  // FF: y reference (= y0) of this lane's joint, loaded once
+  double yq = 0.0, yv = 0.0, yt = 0.0;
+  if (FF) {
+    yq = x0[(long)b * nx + ji];
+    yv = x0[(long)b * nx + 7 + ji];
+    yt = x0[(long)b * nx + 14 + ji];
+  }
   // predicted state (lane-local joint components)
   double hq = J ? x0[(long)b * nx + ji] : 0.0;
   double hv = J ? x0[(long)b * nx + 7 + ji] : 0.0;
@@ -1198,7 +1208,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
           if (FF) acc -= pK[14 + m] * g8_get(dtt, m);
         }
         // crocoddyl order: sum over x components 0..nx-1 (q then v then tau); rounding-level difference only
-        if (C.use_box) acc = fmin(fmax(acc, C.u_lb[ji]), C.u_ub[ji]);
+        if (C.use_box) acc = fmin(fmax(acc, K.ulb), K.uub);
         u = acc;
         if (J) utr[(long)t * NU + ji] = u;
       }
@@ -1206,7 +1216,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
       double qn, vn, cp, lam[3];
       const double uin = FF ? xt_t : u;
       PP(8);
-      node_calc_g8<NC>(C, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam
+      node_calc_g8<NC>(C, K, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam
 #ifdef FFDDP_PHASE_PROF
                        , pp_acc, pp_last
 #endif
@@ -1216,10 +1226,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
       if (FF) {
         tn = C.alpha * xt_t + C.beta * u;
         if (J) {
-          const double e1 = xq_t - yref[ji], e2 = xv_t - yref[7 + ji], e3 = xt_t - yref[14 + ji];
-          c += 0.5 * C.w_y * (C.Wy2[ji] * e1 * e1 + C.Wy2[7 + ji] * e2 * e2 + C.Wy2[14 + ji] * e3 * e3);
+          const double e1 = xq_t - yq, e2 = xv_t - yv, e3 = xt_t - yt;
+          c += 0.5 * C.w_y * (K.wy2q * e1 * e1 + K.wy2v * e2 * e2 + K.wy2t * e3 * e3);
           c += 0.5 * C.w_w * u * u;
-          const double ov = fabs(u) - C.ws_lim[ji];
+          const double ov = fabs(u) - K.wslim;
           const double oo = ov > 0.0 ? ov : 0.0;
           c += C.w_ws * (0.5 * oo * oo);
         }
@@ -1237,15 +1247,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
       double qn, vn, cp, lam[3];
       const int mode = FF ? MODE_TERMINAL_U : MODE_TERMINAL_X;
       PP(8);
-      node_calc_g8<NC>(C, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam
+      node_calc_g8<NC>(C, K, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam
 #ifdef FFDDP_PHASE_PROF
                        , pp_acc, pp_last
 #endif
       );
       double c = FF ? C.dt * cp : cp;
       if (FF && J) {
-        const double e1 = xq_t - yref[ji], e2 = xv_t - yref[7 + ji], e3 = xt_t - yref[14 + ji];
-        c += 0.5 * C.w_y * (C.Wy2[ji] * e1 * e1 + C.Wy2[7 + ji] * e2 * e2 + C.Wy2[14 + ji] * e3 * e3);
+        const double e1 = xq_t - yq, e2 = xv_t - yv, e3 = xt_t - yt;
+        c += 0.5 * C.w_y * (K.wy2q * e1 * e1 + K.wy2v * e2 * e2 + K.wy2t * e3 * e3);
       }
       cost += g8_sum(c);
       if (bad(cost)) fail = true;
