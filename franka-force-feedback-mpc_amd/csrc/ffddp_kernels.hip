@@ -496,6 +496,7 @@ template <bool FF> struct BwW {
   double Vx[NX], Qv[ND], kk[NU], z[NU];
   double fs[64], kp[64], uu[64], ulb[64], uub[64];  // one slot per lane: written without lane guards
   int flag;
+  int badw[2];  // k_backward_w2: per-wave NaN flags of phases F / G
   int clamped[NU];
 };
 
@@ -692,7 +693,7 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
 // waves fit one per SIMD), the other one's blocks exit at once.
 template <bool FF, bool LATE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (FF ? 2 : BW_WAVES)))) void k_backward_w(
-    const DevConsts* __restrict__ Cg, Dev d, int iter, int cur, int late_max) {
+    const DevConsts* __restrict__ Cg, Dev d, int iter, int cur, int late_max, int w2_max) {
   using S_t = BwW<FF>;
   constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
   constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane
@@ -701,7 +702,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   const int l = threadIdx.x;
   if (blockIdx.x == 0 && l == 0) d.acnt[cur ^ 1] = 0;  // the list k_accept builds
   const ActiveList al = active_list(d, cur);
-  if ((int)blockIdx.x >= al.n || (LATE ? al.n > late_max : al.n <= late_max)) return;
+  // active-count ranges: (late_max, B] this variant, (w2_max, late_max] LATE,
+  // [1, w2_max] the two-wave k_backward_w2
+  if ((int)blockIdx.x >= al.n || (LATE ? (al.n > late_max || al.n <= w2_max) : al.n <= late_max)) return;
   const int b = al.list[blockIdx.x];
   InstState* st = d.st + b;
   if (st->done) return;
@@ -1042,6 +1045,387 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
     st->n_retries += retries;
     // the trial k_node read in place has been written into (xs, us): no
     // later kernel may take it for the current iterate (k_commit)
+    st->accepted = -1;
+    if (fail_inst) {
+      st->bw_ok = 0;
+      st->iter = iter;
+      st->done = 1;
+      st->ok = 0;
+      st->n_backward += retries;
+    } else {
+      st->dg = dg;
+      st->dq = dq;
+      st->stop = stop;
+      st->ffeas = ffl;
+      st->bw_ok = 1;
+      st->n_backward += retries + 1;
+      st->n_iters += 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_backward_w2: the backward pass on TWO wavefronts per instance, for slices
+// whose active instances fit two waves per SIMD-pair (the latency-bound
+// end of a solve and small per-GPU batches).  Same per-entry arithmetic as
+// k_backward_w (bit-identical results), spread over 128 lanes:
+//   A, B, C, F  the entry-parallel phases on both waves (half the passes),
+//   D           gains on wave 0 (rows on lanes 0..6) while wave 1 stages the
+//               next node's record into LDS (S.R is dead after phase C) and
+//               issues the prefetch of the one after,
+//   E, G        wave 0 (one column / state component per lane, as before).
+// ---------------------------------------------------------------------------
+template <bool FF>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k_backward_w2(
+    const DevConsts* __restrict__ Cg, Dev d, int iter, int cur, int w2_max) {
+  using S_t = BwW<FF>;
+  constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
+  constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane of wave 1
+  const DevConsts& C = *Cg;
+  const int N = C.N;
+  const int tid = threadIdx.x;
+  const int wv = tid >> 6, l = tid & 63;
+  if (blockIdx.x == 0 && tid == 0) d.acnt[cur ^ 1] = 0;  // the list k_accept builds
+  const ActiveList al = active_list(d, cur);
+  if ((int)blockIdx.x >= al.n || al.n > w2_max) return;
+  const int b = al.list[blockIdx.x];
+  InstState* st = d.st + b;
+  if (st->done) return;
+  __shared__ S_t S;
+  const bool feas = st->is_feasible != 0;
+  const bool use_qp = C.use_box && feas;
+  const double dt = C.dt, dt2 = C.dt * C.dt, alpha = C.alpha, beta = C.beta;
+  const double* recb = d.rec_buf + (long)b * (N + 1) * REC;
+  if (st->recalc && wv == 0) {
+    double c = 0.0;
+    for (int t = l; t <= N; t += 64) c += recb[(long)t * REC + rec_off_cost(NX)];
+    c = wave_sum(c);
+    if (l == 0) {
+      st->cost = c;
+      st->n_calc += 1;
+    }
+  }
+  double preg = st->preg;
+  int retries = 0;
+  bool fail_inst = false;
+  double dg = 0.0, dq = 0.0, stop = 0.0, ffl = 0.0;
+  if (wv == 0) {
+    S.ulb[l] = C.u_lb[l < NU ? l : NU - 1];
+    S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
+  }
+  // this lane's lower-triangle entries of Q (phase C) and V (phase F) over 128 lanes
+  constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 127) / 128;
+  constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 127) / 128;
+  int qrc[NQL], vij[NVL];
+#pragma unroll
+  for (int k = 0; k < NQL; ++k) {
+    int r = 0, c = 0;
+    if (tid + 128 * k < NQE) tri_rc(tid + 128 * k, r, c);
+    qrc[k] = (r << 8) | c;
+  }
+#pragma unroll
+  for (int k = 0; k < NVL; ++k) {
+    int i = 0, j = 0;
+    if (tid + 128 * k < NVE) tri_rc(tid + 128 * k, i, j);
+    vij[k] = (i << 8) | j;
+  }
+  const int lx = l < NX ? l : NX - 1, lu = l < NU ? l : NU - 1;
+  for (;;) {
+    dg = dq = stop = ffl = 0.0;
+    bool failed = false;
+    // ---- terminal node: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N) ----
+    {
+      const double* rT = recb + (long)N * REC;
+      for (int e = tid; e < NX * NX; e += 128) {
+        const int i = e / NX, j = e % NX;
+        S.V[e] = rT[rec_off_Lxx(NX) + e] + (i == j ? preg : 0.0);
+      }
+      if (wv == 0) S.fs[l] = d.fs[((long)b * (N + 1) + N) * NX + lx];
+    }
+    // wave 1: record N-1 into LDS now, the prefetch of record N-2 in flight
+    double pf[NPF];
+    if (wv == 1) {
+      const double* r1 = recb + (long)(N - 1) * REC;
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
+      const double* r2 = recb + (long)(N > 1 ? N - 2 : 0) * REC;
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) pf[k] = r2[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
+    }
+    lds_sync();
+    double pfs = 0.0, pkp = 0.0, pus = 0.0;
+    if (wv == 0) {
+      pfs = d.fs[((long)b * (N + 1) + N - 1) * NX + lx];
+      pkp = d.k[((long)b * N + N - 1) * NU + lu];
+      pus = d.us[((long)b * N + N - 1) * NU + lu];
+      double cdg = 0.0, cdq = 0.0;
+      if (l < NX) {
+        const double* rT = recb + (long)N * REC;
+        double vfs = 0.0;
+        for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
+        const double fj = S.fs[l];
+        ffl = fabs(fj);
+        const double vx = rT[rec_off_Lx(NX) + l] + (feas ? 0.0 : vfs);
+        if (!feas) {
+          d.w[((long)b * (N + 1) + N) * NX + l] = vfs;
+          cdg = -vx * fj;
+          cdq = fj * vfs;
+        }
+        S.Vx[l] = vx;
+      }
+      dg += cdg;
+      dq += cdq;
+    }
+    lds_sync();
+    for (int t = N - 1; t >= 0; --t) {
+      // ---- wave 0: this node's gap / warm start / control (record t is in LDS) ----
+      if (wv == 0) {
+        S.fs[l] = pfs;
+        S.kp[l] = pkp;
+        S.uu[l] = pus;
+        const int tn = t > 0 ? t - 1 : 0;
+        pfs = d.fs[((long)b * (N + 1) + tn) * NX + lx];
+        pkp = d.k[((long)b * N + tn) * NU + lu];
+        pus = d.us[((long)b * N + tn) * NU + lu];
+      }
+      const double* Ar = S.R + rec_off_A();
+      // ---- phase A: W = V D (NX x 7), Y = D' V D (7 x 7), z = D' Vx ----
+      for (int e = tid; e < NX * NU; e += 128) {
+        const int i = e / NU, m = e - (e / NU) * NU;
+        S.W[e] = dt2 * S.V[i * NX + m] + dt * S.V[i * NX + 7 + m];
+      }
+      if (tid >= 128 - NU * NU) {
+        const int e = tid - (128 - NU * NU);
+        const int m = e / NU, n = e - (e / NU) * NU;
+        const double wq = dt2 * S.V[m * NX + n] + dt * S.V[m * NX + 7 + n];
+        const double wv_ = dt2 * S.V[(7 + m) * NX + n] + dt * S.V[(7 + m) * NX + 7 + n];
+        S.Y[e] = dt2 * wq + dt * wv_;
+      }
+      if (tid < NU) S.z[tid] = dt2 * S.Vx[tid] + dt * S.Vx[7 + tid];
+      lds_sync();
+      // ---- phase B: row c of M = I~'W + 1/2 A^'Y (columns m split over the
+      // two waves) ; Qv[c] = [Lx; Lu] + I~'Vx + A^'z (wave 1) ----
+      if (l < ND) {
+        const int c = l;
+        int r0, r1;
+        double a0, a1;
+        itilde2<FF>(c, dt, alpha, beta, r0, a0, r1, a1);
+        const double ac = (FF && c >= 21) ? 0.0 : 1.0;
+        const int cc = (FF && c >= 21) ? 0 : c;
+        double Acol[NU];
+#pragma unroll
+        for (int n = 0; n < NU; ++n) Acol[n] = ac * Ar[cc * 7 + n];
+        const int m0 = wv == 0 ? 0 : 4, m1 = wv == 0 ? 4 : NU;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) {
+          if (m < m0 || m >= m1) continue;
+          double h = 0.0;
+#pragma unroll
+          for (int n = 0; n < NU; ++n) h += Acol[n] * S.Y[n * NU + m];
+          S.M[c * NU + m] = (a0 * S.W[r0 * NU + m] + a1 * S.W[r1 * NU + m]) + 0.5 * h;
+        }
+        if (wv == 1) {
+          double qv = (c < NX) ? S.R[rec_off_Lx(NX) + c] : S.R[rec_off_Lu(NX) + c - NX];
+          qv += a0 * S.Vx[r0] + a1 * S.Vx[r1];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) qv += Acol[m] * S.z[m];
+          S.Qv[c] = qv;
+        }
+      }
+      lds_sync();
+      // ---- phase C: Q lower triangle (mirrored), entries over 128 lanes ----
+#pragma unroll
+      for (int k = 0; k < NQL; ++k) {
+        if (tid + 128 * k < NQE) {
+          const int r = qrc[k] >> 8, c = qrc[k] & 255;
+          double lv;
+          if (r < NX)
+            lv = S.R[rec_off_Lxx(NX) + r * NX + c];
+          else if (c < NX)
+            lv = S.R[rec_off_Lxu(NX) + c * NU + (r - NX)];
+          else
+            lv = S.R[rec_off_Luu(NX) + (r - NX) * NU + (c - NX)];
+          int rr0, rr1, cr0, cr1;
+          double ra0, ra1, ca0, ca1;
+          itilde2<FF>(r, dt, alpha, beta, rr0, ra0, rr1, ra1);
+          itilde2<FF>(c, dt, alpha, beta, cr0, ca0, cr1, ca1);
+          const double g = ra0 * (ca0 * S.V[rr0 * NX + cr0] + ca1 * S.V[rr0 * NX + cr1]) +
+                           ra1 * (ca0 * S.V[rr1 * NX + cr0] + ca1 * S.V[rr1 * NX + cr1]);
+          const double sr = (FF && r >= 21) ? 0.0 : 1.0, sc = (FF && c >= 21) ? 0.0 : 1.0;
+          const int ir = (FF && r >= 21) ? 0 : r, ic = (FF && c >= 21) ? 0 : c;
+          double h1 = 0.0, h2 = 0.0;
+#pragma unroll
+          for (int m = 0; m < NU; ++m) {
+            h1 += S.M[r * NU + m] * Ar[ic * 7 + m];
+            h2 += S.M[c * NU + m] * Ar[ir * 7 + m];
+          }
+          double v = lv + g + (sc * h1 + sr * h2);
+          if (r == c && r >= NX) v += preg;
+          S.Q[r * ND + c] = v;
+          S.Q[c * ND + r] = v;
+          if (c >= NX) {
+            S.H[(r - NX) * NU + (c - NX)] = v;
+            S.H[(c - NX) * NU + (r - NX)] = v;
+          }
+        }
+      }
+      lds_sync();
+      // ---- phase D: gains on wave 0 (rows on lanes 0..6); wave 1 stages the
+      // next node's record (S.R is not read after phase C) ----
+      if (wv == 0) {
+        double hrow[NU], Lr[NU];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.H[l * NU + j] : (l == j ? 1.0 : 0.0);
+        bool ok;
+        if (!use_qp) {
+#pragma unroll
+          for (int j = 0; j < NU; ++j) Lr[j] = hrow[j];
+          ok = chol_rows(Lr, l);
+          if (l < NU) S.clamped[l] = 0;
+        } else {
+          const bool v = l < NU;
+          const double q = v ? S.Qv[NX + l] : 0.0;
+          const double lb = v ? S.ulb[l] - S.uu[l] : 0.0;
+          const double ub = v ? S.uub[l] - S.uu[l] : 0.0;
+          double x = v ? S.kp[l] : 0.0;
+          int clm = 0;
+          ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l);
+          if (ok && v) {
+            const bool c = (clm >> l) & 1;
+            S.kk[l] = -x;
+            S.clamped[l] = c ? 1 : 0;
+            if (c) S.Qv[NX + l] = 0.0;  // BoxFDDP: clamped Qu entries are zeroed
+          }
+        }
+        if (ok && l < NU)
+#pragma unroll
+          for (int j = 0; j < NU; ++j)
+            if (j <= l) S.L[tri(l, j)] = Lr[j];
+        if (l == 0) S.flag = ok ? 1 : 0;
+      } else if (t > 0) {
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
+        const int tn = t > 1 ? t - 2 : 0;
+        const double* r1 = recb + (long)tn * REC;
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
+      }
+      lds_sync();
+      if (S.flag == 0) {
+        failed = true;
+        break;
+      }
+      // ---- phase E: K columns (and k for LLT), wave 0 ----
+      if (wv == 0 && (l < NX || (!use_qp && l == NX))) {
+        double col[NU];
+        if (l < NX) {
+#pragma unroll
+          for (int c = 0; c < NU; ++c) col[c] = S.clamped[c] ? 0.0 : S.Q[l * ND + NX + c];
+        } else {
+#pragma unroll
+          for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
+        }
+        chol_solve<NU>(S.L, col);
+        if (l < NX) {
+          double* Kt = d.K + ((long)b * N + t) * NU * NX;
+#pragma unroll
+          for (int c = 0; c < NU; ++c) {
+            S.K[c * NX + l] = col[c];
+            Kt[c * NX + l] = col[c];
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < NU; ++c) S.kk[c] = col[c];
+        }
+      }
+      lds_sync();
+      // ---- phase F: Vxx = sym(Qxx - Qxu K) + preg I, entries over 128 lanes ----
+      int badv = 0;
+#pragma unroll
+      for (int k = 0; k < NVL; ++k) {
+        if (tid + 128 * k >= NVE) continue;
+        const int i = vij[k] >> 8, j = vij[k] & 255;
+        double a1 = 0.0, a2 = 0.0;
+#pragma unroll
+        for (int c = 0; c < NU; ++c) {
+          a1 += S.Q[i * ND + NX + c] * S.K[c * NX + j];
+          a2 += S.Q[j * ND + NX + c] * S.K[c * NX + i];
+        }
+        const double v = S.Q[i * ND + j] - 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
+        S.V[i * NX + j] = v;
+        S.V[j * NX + i] = v;
+        badv |= bad(fabs(v)) ? 1 : 0;
+      }
+      if (wv == 1) {
+        badv = __any(badv);
+        if (l == 0) S.badw[1] = badv;
+      }
+      lds_sync();
+      // ---- phase G: Vx, gap terms, expected improvement, k (wave 0) ----
+      double cdg = 0.0, cdq = 0.0, cst = 0.0;
+      if (wv == 0) {
+        if (l < NX) {
+          double vfs = 0.0;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
+          double vx = S.Qv[l];
+#pragma unroll
+          for (int c = 0; c < NU; ++c) vx -= S.K[c * NX + l] * S.Qv[NX + c];
+          if (!feas) vx += vfs;
+          badv |= bad(fabs(vx)) ? 1 : 0;
+          ffl = fmax(ffl, fabs(S.fs[l]));
+          if (!feas) {
+            d.w[((long)b * (N + 1) + t) * NX + l] = vfs;
+            cdg -= vx * S.fs[l];
+            cdq += S.fs[l] * vfs;
+          }
+          if (l < NU) {
+            double quk = 0.0;
+#pragma unroll
+            for (int m = 0; m < NU; ++m) quk += S.H[l * NU + m] * S.kk[m];
+            const double qu = S.Qv[NX + l], kl = S.kk[l];
+            cdg += qu * kl;
+            cdq -= kl * quk;
+            cst += qu * qu;
+            d.k[((long)b * N + t) * NU + l] = kl;
+          }
+          S.Vx[l] = vx;  // old Vx is dead after phase B
+        }
+        badv = __any(badv);
+        if (l == 0) S.badw[0] = badv;
+      }
+      lds_sync();
+      if (S.badw[0] | S.badw[1]) {
+        failed = true;
+        break;
+      }
+      dg += cdg;
+      dq += cdq;
+      stop += cst;
+    }
+    // ---- retry bookkeeping (SolverFDDP::solve: increaseRegularization) ----
+    if (!failed) {
+      if (wv == 0) {
+        dg = wave_sum(dg);
+        dq = wave_sum(dq);
+        stop = wave_sum(stop);
+        ffl = wave_max(ffl);
+      }
+      break;
+    }
+    retries++;
+    preg = fmin(preg * C.reg_inc, C.reg_max);
+    if (preg == C.reg_max) {
+      fail_inst = true;
+      break;
+    }
+    lds_sync();
+  }
+  if (tid == 0) {
+    st->preg = preg;
+    st->n_retries += retries;
     st->accepted = -1;
     if (fail_inst) {
       st->bw_ok = 0;
@@ -1644,6 +2028,7 @@ struct ffddp_handle {
   std::vector<int> fw_sched{2, 2, 2, 2};
   int bw_late_max = -1;  // active instances up to which a slice's backward pass uses the latency variant
                          // (FFDDP_BW_LATE_MAX; -1: SIMDs / slices)
+  int bw_w2_max = -1;    // ... and the two-wave variant (FFDDP_BW_W2_MAX; -1: SIMDs / (2 slices); 0: never)
   int n_simd = 1024;     // SIMDs of the device (4 per CU)
   bool fw_fill = true;   // widen the first line-search pass to fill the SIMDs (FFDDP_FW_FILL=0: off)
   // optional per-kernel timing
@@ -1831,10 +2216,20 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       {
         ProfScope p(h, ss, KC_BACKWARD);
         const int lmax = h->bw_late_max >= 0 ? h->bw_late_max : h->n_simd / S;
-        if (lmax < Bk) hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1, lmax);
-        if (lmax > 0)
+        // two-wave variant: for slices no larger than one wave per SIMD share
+        // (small per-GPU batches, where the whole solve is latency-bound); in
+        // the tail of large slices the other slices' kernels hold the SIMDs and
+        // its 2-wave blocks wait for them (B = 4096: -1.7 %)
+        const int w2auto = Bk <= h->n_simd / S ? h->n_simd / (2 * S) : 0;
+        const int w2max = std::min(lmax, h->bw_w2_max >= 0 ? h->bw_w2_max : w2auto);
+        if (lmax < Bk)
+          hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1, lmax, w2max);
+        if (lmax > w2max && w2max < Bk)
           hipLaunchKernelGGL((k_backward_w<FF, true>), dim3(lmax < Bk ? lmax : Bk), dim3(64), 0, ss, h->dc, d, it, it & 1,
-                             lmax);
+                             lmax, w2max);
+        if (w2max > 0)
+          hipLaunchKernelGGL((k_backward_w2<FF>), dim3(w2max < Bk ? w2max : Bk), dim3(128), 0, ss, h->dc, d, it, it & 1,
+                             w2max);
       }
       int n1 = NTRIALS;
       {
@@ -2053,6 +2448,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
       h->nstreams = v < 1 ? 1 : (v > 8 ? 8 : v);
     }
     if (const char* bl = std::getenv("FFDDP_BW_LATE_MAX")) h->bw_late_max = std::atoi(bl);
+    if (const char* bw2 = std::getenv("FFDDP_BW_W2_MAX")) h->bw_w2_max = std::atoi(bw2);
     if (const char* ff = std::getenv("FFDDP_FW_FILL")) h->fw_fill = std::atoi(ff) != 0;
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
       h->fw_sched.clear();

@@ -378,6 +378,7 @@ ENV_VARIANTS = [
     {"FFDDP_FW_SCHED": "1,3,5"}, {"FFDDP_FW_SCHED": "10"}, {"FFDDP_FW_FIRST": "1"}, {"FFDDP_STAGGER": "0"},
     {"FFDDP_STAGGER": "1"}, {"FFDDP_CALLER_SLICE": "0"}, {"FFDDP_STREAMS": "2"}, {"FFDDP_STREAMS": "3"},
     {"FFDDP_STREAMS": "8"}, {"FFDDP_BW_LATE_MAX": "0"}, {"FFDDP_BW_LATE_MAX": "100000"}, {"FFDDP_FW_FILL": "0"},
+    {"FFDDP_BW_W2_MAX": "0"}, {"FFDDP_BW_W2_MAX": "100000"},
 ]
 
 
@@ -408,7 +409,7 @@ def test_launch_settings_bit_identical(variant, monkeypatch):
 # the latency variant of the backward pass and a single 10-step-length line
 # search pass): the same solves through the 2-waves/SIMD backward variant and
 # through the two-pass line search (2 step lengths first, the rest second).
-@pytest.mark.parametrize("env", [{"FFDDP_BW_LATE_MAX": "0"}, {"FFDDP_FW_FILL": "0"},
+@pytest.mark.parametrize("env", [{"FFDDP_BW_LATE_MAX": "0"}, {"FFDDP_BW_W2_MAX": "0"}, {"FFDDP_FW_FILL": "0"},
                                  {"FFDDP_BW_LATE_MAX": "0", "FFDDP_FW_FILL": "0", "FFDDP_FW_FIRST": "2"}])
 @pytest.mark.parametrize("variant", ["classical", "ff"])
 def test_solve_schedule_variants(variant, env, monkeypatch):
