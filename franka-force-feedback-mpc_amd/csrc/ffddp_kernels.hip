@@ -104,6 +104,20 @@ __device__ __forceinline__ ActiveList active_list(const Dev& d, int cur) {
   return ActiveList{d.alist + (long)cur * d.B, d.acnt[cur]};
 }
 
+// XCD-aware block order.  The hardware hands consecutive workgroups to the 8
+// XCDs round-robin, each XCD with its own L2: an instance's node groups (or
+// line-search trials) spread over several blocks would pull its shared lines
+// (node references, the iterate, K, the instance state, partly written gap
+// lines) into several L2s.  Remap so that each XCD processes one contiguous
+// range of the n blocks that carry work; blocks >= n keep their index.
+constexpr int N_XCD = 8;
+__device__ __forceinline__ long xcd_block(long b, long n) {
+  if (b >= n) return b;
+  const long q = n / N_XCD, r = n % N_XCD;
+  const long x = b % N_XCD, i = b / N_XCD;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 // ---------------------------------------------------------------------------
 // init
 // ---------------------------------------------------------------------------
@@ -288,7 +302,9 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
   constexpr int nc = NC;
   __shared__ NodeShared S;
   const int grp = threadIdx.x / NODE_GROUP, lane = threadIdx.x % NODE_GROUP;
-  const long gnode = (long)blockIdx.x * NODE_GPB + grp;
+  const int n_work = force_all ? d.B : d.acnt[cur];  // instances with nodes to evaluate
+  const long blk = xcd_block(blockIdx.x, ((long)n_work * (N + 1) + NODE_GPB - 1) / NODE_GPB);
+  const long gnode = blk * NODE_GPB + grp;
   const int slot = (int)(gnode / (N + 1)), t = (int)(gnode % (N + 1));
   int b = slot;
   bool active = slot < d.B;
@@ -1091,6 +1107,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
   const int b = al.list[blockIdx.x];
   InstState* st = d.st + b;
   if (st->done) return;
+#ifdef FFDDP_PHASE_PROF
+  const bool pp_on = (b == 0) && tid == 0;
+#endif
+  PP_INIT();
   __shared__ S_t S;
   const bool feas = st->is_feasible != 0;
   const bool use_qp = C.use_box && feas;
@@ -1190,6 +1210,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
         pkp = d.k[((long)b * N + tn) * NU + lu];
         pus = d.us[((long)b * N + tn) * NU + lu];
       }
+      PP(0);
       const double* Ar = S.R + rec_off_A();
       // ---- phase A: W = V D (NX x 7), Y = D' V D (7 x 7), z = D' Vx ----
       for (int e = tid; e < NX * NU; e += 128) {
@@ -1205,6 +1226,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
       }
       if (tid < NU) S.z[tid] = dt2 * S.Vx[tid] + dt * S.Vx[7 + tid];
       lds_sync();
+      PP(1);
       // ---- phase B: row c of M = I~'W + 1/2 A^'Y (columns m split over the
       // two waves) ; Qv[c] = [Lx; Lu] + I~'Vx + A^'z (wave 1) ----
       if (l < ND) {
@@ -1235,6 +1257,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
         }
       }
       lds_sync();
+      PP(2);
       // ---- phase C: Q lower triangle (mirrored), entries over 128 lanes ----
 #pragma unroll
       for (int k = 0; k < NQL; ++k) {
@@ -1272,6 +1295,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
         }
       }
       lds_sync();
+      PP(3);
       // ---- phase D: gains on wave 0 (rows on lanes 0..6); wave 1 stages the
       // next node's record (S.R is not read after phase C) ----
       if (wv == 0) {
@@ -1313,6 +1337,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
         for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
       }
       lds_sync();
+      PP(4);
       if (S.flag == 0) {
         failed = true;
         break;
@@ -1341,6 +1366,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
         }
       }
       lds_sync();
+      PP(5);
       // ---- phase F: Vxx = sym(Qxx - Qxu K) + preg I, entries over 128 lanes ----
       int badv = 0;
 #pragma unroll
@@ -1363,6 +1389,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
         if (l == 0) S.badw[1] = badv;
       }
       lds_sync();
+      PP(6);
       // ---- phase G: Vx, gap terms, expected improvement, k (wave 0) ----
       double cdg = 0.0, cdq = 0.0, cst = 0.0;
       if (wv == 0) {
@@ -1397,6 +1424,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
         if (l == 0) S.badw[0] = badv;
       }
       lds_sync();
+      PP(7);
       if (S.badw[0] | S.badw[1]) {
         failed = true;
         break;
@@ -1423,6 +1451,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
     }
     lds_sync();
   }
+  PP_FLUSH();
   if (tid == 0) {
     st->preg = preg;
     st->n_retries += retries;
@@ -1491,7 +1520,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
   const DevConsts& C = *Cg;
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
-  const long gid = (blockIdx.x * (long)blockDim.x + threadIdx.x) / G8;
+  const long blk = xcd_block(blockIdx.x, ((long)d.acnt[cur] * ntr * G8 + 63) / 64);
+  const long gid = (blk * (long)blockDim.x + threadIdx.x) / G8;
   const int li = g8_lane();
   const bool J = li < NQ;
   const int ji = J ? li : 0;
