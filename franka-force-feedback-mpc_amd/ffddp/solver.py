@@ -132,6 +132,23 @@ class BatchedBoxFDDP:
             raise FfddpError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
 
     # -- solve (host arrays) ----------------------------------------------------------
+    def pinned_batch(self, batch):
+        """A copy of `batch`'s solve inputs in page-locked host memory
+        (ffddp_host_alloc): solve() then copies them by DMA per slice on the
+        slice streams, overlapping the other slices' kernels, instead of
+        staging them.  For callers that refill the same input arrays every
+        tick."""
+        import types
+
+        B, N, nx = int(batch.x0.shape[0]), self.N, self.nx
+        specs = dict(x0=((B, nx), np.float64), node_ref=((B, N + 1, 6), np.float64),
+                     inst_ref=((B, 21), np.float64), surface=((B,), np.uint8),
+                     xs_init=((B, N + 1, nx), np.float64), us_init=((B, N, 7), np.float64))
+        o = _abi.pinned_arrays(specs)
+        for k, (shape, dt) in specs.items():
+            o[k][...] = np.asarray(getattr(batch, k), dt).reshape(shape)
+        return types.SimpleNamespace(**o)
+
     def solve(self, batch, maxiter: int = 10, is_feasible: bool = False, xs_init=None, us_init=None):
         """batch: workload.Batch (or any object with x0, node_ref, inst_ref, surface,
         xs_init, us_init).  Returns ok (B,) bool."""

@@ -86,6 +86,11 @@ def test_pinned_outputs_bit_identical():
     first = p.xs
     p.solve(batch.slice(slice(0, B)), maxiter=10)  # same buffers, overwritten in place
     assert p.xs is first
+    # page-locked inputs as well (per-slice DMA of the inputs, no staging)
+    pin = p.pinned_batch(batch)
+    p.solve(pin, maxiter=10)
+    for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred", "stats"):
+        assert np.array_equal(getattr(a, name), getattr(p, name), equal_nan=True), name
     a.close()
     p.close()
 
