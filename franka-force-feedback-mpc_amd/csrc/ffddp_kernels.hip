@@ -588,7 +588,10 @@ __device__ __forceinline__ double rowb(double v, int k) {
 
 // In-place LLT of the SPD matrix whose row i is held by lane i: on exit
 // a[j] (j < i) = L_ij and a[i] = 1 / L_ii (same operation order as
-// chol_packed).  Returns false (uniformly) at the first non-positive pivot.
+// chol_packed).  Returns false (uniformly) if a pivot is not positive.  The
+// pivot test is one ballot after the factorisation, not a branch per pivot:
+// past a bad pivot the values are garbage (NaN) but unused, and a good
+// factorisation takes the same operations either way.
 __device__ __forceinline__ bool chol_rows(double (&a)[NU], int lane) {
 #pragma unroll
   for (int k = 0; k < NU; ++k) {
@@ -1482,13 +1485,33 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
 // ---------------------------------------------------------------------------
 // SolverFDDP::solve acceptance of trial tr (tryStep + expectedImprovement)
 // for an instance in state s; dV / dVexp / d1 of the trial out (trace)
-__device__ __forceinline__ bool trial_accepted(const DevConsts& C, const Dev& d, const InstState& s, int b, int tr,
+// the line search's results of instance b, trials 0..n-1, loaded at once
+// (n is NTRIALS or the first pass's width): the acceptance loop below exits
+// at the first accepted trial, and with the loads inside it every trial
+// cost a dependent global-memory round trip
+struct TrialRes {
+  double cost[NTRIALS], dv[NTRIALS];
+  bool fail[NTRIALS];
+};
+__device__ __forceinline__ void load_trials(const Dev& d, int b, int n, TrialRes& T) {
+  const double* tb = d.trial + (long)b * NTRIALS * 2;
+  const int* fb = d.trial_fail + (long)b * NTRIALS;
+#pragma unroll
+  for (int tr = 0; tr < NTRIALS; ++tr) {
+    const bool in = tr < n;
+    T.cost[tr] = in ? tb[2 * tr] : 0.0;
+    T.dv[tr] = in ? tb[2 * tr + 1] : 0.0;
+    T.fail[tr] = in ? fb[tr] != 0 : true;
+  }
+}
+
+__device__ __forceinline__ bool trial_accepted(const DevConsts& C, const InstState& s, const TrialRes& T, int tr,
                                                double* o_dV = nullptr, double* o_dVexp = nullptr,
                                                double* o_d1 = nullptr) {
-  if (d.trial_fail[(long)b * NTRIALS + tr]) return false;
+  if (T.fail[tr]) return false;
   const double a = C.alphas[tr];
-  const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
-  const double dv = s.is_feasible ? 0.0 : d.trial[((long)b * NTRIALS + tr) * 2 + 1];
+  const double cost_try = T.cost[tr];
+  const double dv = s.is_feasible ? 0.0 : T.dv[tr];
   const double dV = s.cost - cost_try;
   const double d0 = s.dg + dv, d1 = s.dq - 2.0 * dv;
   const double dVexp = a * (d0 + 0.5 * a * d1);
@@ -1539,8 +1562,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
     // second pass of the line search: only instances none of whose first
     // tr0 trials was accepted (the first pass's results are complete: same stream)
     const InstState sv = *st;
+    TrialRes T;
+    load_trials(d, b, tr0, T);
     bool any = false;
-    for (int t2 = 0; t2 < tr0 && !any; ++t2) any = trial_accepted(C, d, sv, b, t2);
+    for (int t2 = 0; t2 < tr0 && !any; ++t2) any = trial_accepted(C, sv, T, t2);
     if (any) return;
   }
 #ifdef FFDDP_PHASE_PROF
@@ -1693,6 +1718,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
 // (-1: none, or the instance is done).
 __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int n1) {
   InstState s = d.st[b];
+  TrialRes T;  // issued with the state load (unused for a done instance)
+  load_trials(d, b, NTRIALS, T);
   if (s.done) {
     d.st[b].accepted = -1;
     return -1;
@@ -1705,9 +1732,9 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int 
   double tdV = __builtin_nan(""), tdVexp = __builtin_nan(""), td1 = __builtin_nan("");
   for (int tr = 0; tr < NTRIALS; ++tr) {
     const double a = C.alphas[tr];
-    const double cost_try = d.trial[((long)b * NTRIALS + tr) * 2 + 0];
+    const double cost_try = T.cost[tr];
     double e0 = tdV, e1 = tdVexp, e2 = td1;
-    const bool okt = trial_accepted(C, d, s, b, tr, &e0, &e1, &e2);
+    const bool okt = trial_accepted(C, s, T, tr, &e0, &e1, &e2);
     tdV = e0;
     tdVexp = e1;
     td1 = e2;
