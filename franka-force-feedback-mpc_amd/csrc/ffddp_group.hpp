@@ -275,19 +275,22 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, const LaneK& K,
     for (int k = 0; k < 9; ++k) Rp[k] = g8_up(R[k], d);
 #pragma unroll
     for (int k = 0; k < 3; ++k) op[k] = g8_up(o[k], d);
-    if (li >= d) {
-      double Rn[9], on[3];
+    // composed on every lane, kept where the source lane is in the group: a
+    // select per value instead of an exec-masked block, whose results the
+    // compiler copied out of and back into the loop-carried registers
+    // (two moves per value and step)
+    const bool take = li >= d;
+    double Rn[9], on[3];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < 3; ++r) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) Rn[3 * r + c] = Rp[3 * r + 0] * R[c] + Rp[3 * r + 1] * R[3 + c] + Rp[3 * r + 2] * R[6 + c];
-        on[r] = op[r] + (Rp[3 * r + 0] * o[0] + Rp[3 * r + 1] * o[1] + Rp[3 * r + 2] * o[2]);
-      }
-#pragma unroll
-      for (int k = 0; k < 9; ++k) R[k] = Rn[k];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) o[k] = on[k];
+      for (int c = 0; c < 3; ++c) Rn[3 * r + c] = Rp[3 * r + 0] * R[c] + Rp[3 * r + 1] * R[3 + c] + Rp[3 * r + 2] * R[6 + c];
+      on[r] = op[r] + (Rp[3 * r + 0] * o[0] + Rp[3 * r + 1] * o[1] + Rp[3 * r + 2] * o[2]);
     }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = take ? Rn[k] : R[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o[k] = take ? on[k] : o[k];
   }
   // joint axis (world) and spatial motion subspace S = (o x z, z)
   double z[3] = {J ? R[2] : 0.0, J ? R[5] : 0.0, J ? R[8] : 0.0};
@@ -419,9 +422,13 @@ __device__ __forceinline__ void node_calc_g8(const DevConsts& C, const LaneK& K,
   double a = 0.0;
   if (with_dyn) {
     // ---- link forces (RNEA, qdd = 0) and CRBA tuples ----
-    double fl[3] = {0, 0, 0}, fa[3] = {0, 0, 0};
-    double tm = 0.0, th[3] = {0, 0, 0}, tI[6] = {0, 0, 0, 0, 0, 0};
-    if (J) {
+    // every lane, unmasked: lane 7 (the EE frame) has zero mass and inertia
+    // in LaneK, so its link force and CRBA tuple come out zero (its frame
+    // is finite whenever the joint lanes are); an exec-masked block made the
+    // compiler zero-fill and copy the 16 outputs around it
+    double fl[3], fa[3];
+    double tm, th[3], tI[6];
+    {
       const double m = K.m;
       const double* Ic = K.I;
       double cw[3];

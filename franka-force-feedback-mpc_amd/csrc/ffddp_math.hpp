@@ -51,22 +51,37 @@ template <> FFD_HD Dual mk<Dual>(double v, double d) { return {v, d}; }
 // the fdlibm minimax kernels on [-pi/4, pi/4] (< 1 ulp) and fdlibm's rational
 // acos, evaluated branch-free.  Max error vs libm: 2 ulp sin/cos, 1 ulp acos.
 // ---------------------------------------------------------------------------
+// Horner step a * b + k with the coefficient k in an SGPR pair: one
+// v_fma_f64.  The compiler otherwise keeps the coefficients in VGPRs and
+// emits v_fmac_f64 (accumulator tied to the addend) plus a v_mov_b64 copying
+// the coefficient into the accumulator for every step.  Same single rounding
+// as the contracted a * b + k.
+FFD_HD double hfma(double a, double b, double k) {
+#ifdef __HIP_DEVICE_COMPILE__
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+#else
+  return a * b + k;  // host builds (oracle/cpu): the expression as written
+#endif
+}
+
 FFD_HD void sincos_(double x, double& s, double& c) {
   const double n = __builtin_rint(x * 0.63661977236758134308);  // 2 / pi
   double y = fma(-n, 1.5707963267948966, x);                   // pi/2 in three parts
   y = fma(-n, 6.123233995736766e-17, y);
   y = fma(-n, -1.4973849048591698e-33, y);
   const double z = y * y;
-  const double ps = -1.66666666666666324348e-01 +
-                    z * (8.33333333332248946124e-03 +
-                         z * (-1.98412698298579493134e-04 +
-                              z * (2.75573137070700676789e-06 +
-                                   z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10))));
-  const double pc = 4.16666666666666019037e-02 +
-                    z * (-1.38888888888741095749e-03 +
-                         z * (2.48015872894767294178e-05 +
-                              z * (-2.75573143513906633035e-07 +
-                                   z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11))));
+  const double ps = hfma(z, hfma(z, hfma(z, hfma(z, hfma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                                   2.75573137070700676789e-06),
+                                         -1.98412698298579493134e-04),
+                               8.33333333332248946124e-03),
+                     -1.66666666666666324348e-01);
+  const double pc = hfma(z, hfma(z, hfma(z, hfma(z, hfma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                                   -2.75573143513906633035e-07),
+                                         2.48015872894767294178e-05),
+                               -1.38888888888741095749e-03),
+                     4.16666666666666019037e-02);
   const double sp = fma(y * z, ps, y);
   const double cp = fma(z * z, pc, 1.0 - 0.5 * z);
   const int qd = (int)((long long)n & 3);
@@ -80,14 +95,15 @@ FFD_HD double acos_(double x) {
   const double ax = fabs(x);
   const bool mid = ax < 0.5;
   const double z = mid ? x * x : (1.0 - ax) * 0.5;
-  const double p = z * (1.66666666666666657415e-01 +
-                        z * (-3.25565818622400915405e-01 +
-                             z * (2.01212532134862925881e-01 +
-                                  z * (-4.00555345006794114027e-02 +
-                                       z * (7.91534994289814532176e-04 + z * 3.47933107596021167570e-05)))));
-  const double q = 1.0 + z * (-2.40339491173441421878e+00 +
-                              z * (2.02094576023350569471e+00 +
-                                   z * (-6.88283971605453293030e-01 + z * 7.70381505559019352791e-02)));
+  const double p = z * hfma(z, hfma(z, hfma(z, hfma(z, hfma(z, 3.47933107596021167570e-05, 7.91534994289814532176e-04),
+                                                    -4.00555345006794114027e-02),
+                                          2.01212532134862925881e-01),
+                                -3.25565818622400915405e-01),
+                      1.66666666666666657415e-01);
+  const double q = hfma(z, hfma(z, hfma(z, hfma(z, 7.70381505559019352791e-02, -6.88283971605453293030e-01),
+                                        2.02094576023350569471e+00),
+                              -2.40339491173441421878e+00),
+                    1.0);
   const double r = p / q;
   const double pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17;
   if (mid) return pio2_hi - (x - (pio2_lo - x * r));

@@ -79,7 +79,9 @@ __global__ void k(unsigned long long* out, double* sink, double s) {
   double d[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) d[j] = a + j;
-  PIN(a); PIN(b); t0 = clk(); PIN(a);
+  for (int j = 0; j < 8; ++j) PIN(d[j]);
+  t0 = clk();
+  for (int j = 0; j < 8; ++j) PIN(d[j]);
 #pragma unroll
   for (int i = 0; i < N / 8; ++i)
 #pragma unroll
@@ -92,6 +94,82 @@ __global__ void k(unsigned long long* out, double* sink, double s) {
 #pragma unroll
   for (int i = 0; i < N / 8; ++i) a = b / a + 1.0;
   PIN(a); t1 = clk(); out[9] = (t1 - t0) * 8;
+  // 11. 8 independent fp64 FMA chains (issue rate)
+  double e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = a + j;
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+  t0 = clk();
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+#pragma unroll
+  for (int i = 0; i < N / 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = fma(e[j], c, b);
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+  t1 = clk(); out[10] = t1 - t0;
+  for (int j = 0; j < 8; ++j) a += e[j];
+  // 12. 8 independent 64-bit row_newbcast moves (issue rate of v_mov_b64_dpp)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = a + j;
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+  t0 = clk();
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+#pragma unroll
+  for (int i = 0; i < N / 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long long x = __builtin_bit_cast(long long, e[j]);
+      const long long y = __builtin_amdgcn_update_dpp(x, x, 0x153, 0xf, 0xf, true);
+      e[j] = __builtin_bit_cast(double, y);
+    }
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+  t1 = clk(); out[11] = t1 - t0;
+  for (int j = 0; j < 8; ++j) a += e[j];
+  // 13. dependent row_newbcast + add
+  PIN(a); t0 = clk(); PIN(a);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    const long long x = __builtin_bit_cast(long long, a);
+    const long long y = __builtin_amdgcn_update_dpp(x, x, 0x153, 0xf, 0xf, true);
+    a = a + __builtin_bit_cast(double, y);
+  }
+  PIN(a); t1 = clk(); out[12] = (t1 - t0) * 4;
+  // 14. 8 independent v_cndmask-style selects on 64-bit values (per select)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = a + j;
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+  const bool cond = (l & 1) != 0;
+  t0 = clk();
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+#pragma unroll
+  for (int i = 0; i < N / 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { e[j] = cond ? e[j] : b; PIN(e[j]); }
+  t1 = clk(); out[13] = t1 - t0;
+  for (int j = 0; j < 8; ++j) a += e[j];
+  // 15. 8 independent fp64 adds (issue rate)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = a + j;
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+  t0 = clk();
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+#pragma unroll
+  for (int i = 0; i < N / 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = e[j] + b;
+  for (int j = 0; j < 8; ++j) PIN(e[j]);
+  t1 = clk(); out[14] = t1 - t0;
+  for (int j = 0; j < 8; ++j) a += e[j];
+  // 16. dependent g8_bc (two bank-masked newbcast moves) + add
+  PIN(a); t0 = clk(); PIN(a);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    const long long x = __builtin_bit_cast(long long, a);
+    const long long t = __builtin_amdgcn_mov_dpp(x, 0x158 + 3, 0xf, 0xC, false);
+    const long long r = __builtin_amdgcn_update_dpp(t, x, 0x150 + 3, 0xf, 0x3, false);
+    a = a + __builtin_bit_cast(double, r);
+  }
+  PIN(a); t1 = clk(); out[15] = (t1 - t0) * 4;
   sink[l] = a;
 }
 int main() {
@@ -104,7 +182,9 @@ int main() {
   unsigned long long h[16];
   hipMemcpy(h, o, 16 * 8, hipMemcpyDeviceToHost);
   const char* names[] = {"dep fma", "4 indep fma (per fma)", "dpp+add dep", "swizzle bcast+add dep", "readlane bcast+add dep",
-                         "lds st/bar/ld round trip", "dep mul+add (2 ops)", "rsq+add dep", "indep dpp64 (per dpp64)", "div+add dep"};
-  for (int i = 0; i < 10; ++i) printf("%-28s %7.1f cycles per op\n", names[i], (double)h[i] / N);
+                         "lds st/bar/ld round trip", "dep mul+add (2 ops)", "rsq+add dep", "indep dpp64 (per dpp64)", "div+add dep",
+                         "8 indep fma (per fma)", "indep b64 newbcast (per op)", "newbcast+add dep", "select64 (per op)",
+                         "8 indep add (per add)", "g8_bc+add dep"};
+  for (int i = 0; i < 16; ++i) printf("%-28s %7.1f cycles per op\n", names[i], (double)h[i] / N);
   return 0;
 }
