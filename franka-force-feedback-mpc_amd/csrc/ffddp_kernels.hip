@@ -2074,8 +2074,12 @@ struct ffddp_handle {
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
   std::vector<hipEvent_t> stg;  // start-stagger events (FFDDP_STAGGER)
   bool caller_slice = true;  // FFDDP_CALLER_SLICE
-  int stagger = 2;  // 0 off, 1 after the previous slice's first node stage, 2 after its init (the calc is
-                    // fused into k_node, so there is no earlier boundary; 0 / 1 / 2 measure alike)
+  // FFDDP_STAGGER: 0 off, 1 slice k's first node stage after slice k-1's,
+  // 2 after its init; -1 (default) picks per solve: 1 when the slices exceed
+  // one wave per SIMD share (throughput-bound first iterations: B=4096
+  // +2.3 %, B=2048 +4 % over 2), else 0 (latency-bound: the stagger only
+  // delays the last slice, B=512/1024 +1.2 % over 1)
+  int stagger = -1;
   int fw_first = 4;  // trials evaluated before the fallback pass (FFDDP_FW_FIRST)
   // first-pass trial counts of the first iterations (FFDDP_FW_SCHED="2,2,2,2"):
   // while every instance is active the line search is throughput-bound, so a
@@ -2208,6 +2212,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
     }
   }
   const int Bs = (B + S - 1) / S;
+  const int stagger = S == 1 ? 0 : (h->stagger >= 0 ? h->stagger : (Bs > h->n_simd / S ? 1 : 0));
   struct Slice {
     Dev d;
     hipStream_t s;
@@ -2262,14 +2267,14 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       const long nodes = (long)Bk * (N + 1);
       // optional start stagger: slice k's first node stage waits for slice
       // k-1's, so the throughput-bound node stages do not all collide
-      if (it == 0 && k > 0 && h->stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
-      if (it == 0 && h->stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
+      if (it == 0 && k > 0 && stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
+      if (it == 0 && stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_NODE);
         hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, ss,
                            h->dc, d, x0k, nrefk, irefk, surfk, 0, it & 1);
       }
-      if (it == 0 && h->stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
+      if (it == 0 && stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
       {
         ProfScope p(h, ss, KC_BACKWARD);
         const int lmax = h->bw_late_max >= 0 ? h->bw_late_max : h->n_simd / S;

@@ -376,7 +376,7 @@ def test_gravity_torque_dev_matches_oracle():
 # B = 4096 / 517 in tests/test_gpu_batch.py).
 ENV_VARIANTS = [
     {"FFDDP_FW_SCHED": "1,3,5"}, {"FFDDP_FW_SCHED": "10"}, {"FFDDP_FW_FIRST": "1"}, {"FFDDP_STAGGER": "0"},
-    {"FFDDP_STAGGER": "1"}, {"FFDDP_CALLER_SLICE": "0"}, {"FFDDP_STREAMS": "2"}, {"FFDDP_STREAMS": "3"},
+    {"FFDDP_STAGGER": "1"}, {"FFDDP_STAGGER": "2"}, {"FFDDP_CALLER_SLICE": "0"}, {"FFDDP_STREAMS": "2"}, {"FFDDP_STREAMS": "3"},
     {"FFDDP_STREAMS": "8"}, {"FFDDP_BW_LATE_MAX": "0"}, {"FFDDP_BW_LATE_MAX": "100000"}, {"FFDDP_FW_FILL": "0"},
     {"FFDDP_BW_W2_MAX": "0"}, {"FFDDP_BW_W2_MAX": "100000"},
 ]
