@@ -2070,11 +2070,6 @@ struct ffddp_handle {
   // created streams plus the caller's stream, the 4 hardware queues a process
   // gets; FFDDP_CALLER_SLICE=0 puts every slice on a created stream)
   int nstreams = 4;
-  // without FFDDP_STREAMS, a batch of at most one instance per SIMD runs as
-  // one slice: every stage is then a single latency-bound wave per instance,
-  // and four slices only contend (B=1024 224k -> 230k, B=512 133k -> 135k;
-  // from B=1536 on the four slices win)
-  bool streams_auto = true;
   std::vector<hipStream_t> streams;
   std::vector<hipEvent_t> sev;  // fork + per-stream join events
   std::vector<hipEvent_t> stg;  // start-stagger events (FFDDP_STAGGER)
@@ -2202,7 +2197,7 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
                  int32_t* stats, hipStream_t s, HostIO* io) {
   const int N = h->hc.N, nx = h->hc.nx;
   int S = h->nstreams;
-  if (B < 64 * S || (h->streams_auto && B <= h->n_simd)) S = 1;
+  if (B < 64 * S) S = 1;
   if (S > 1 && (int)h->streams.size() < S) {
     if (!stream_pool_acquire(h->device, S, h->streams)) return fail(h, FFDDP_E_DEVICE, "hipStreamCreate failed");
     while ((int)h->sev.size() < S + 1) {
@@ -2513,7 +2508,6 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     if (ns) {
       const int v = std::atoi(ns);
       h->nstreams = v < 1 ? 1 : (v > 8 ? 8 : v);
-      h->streams_auto = false;
     }
     if (const char* bl = std::getenv("FFDDP_BW_LATE_MAX")) h->bw_late_max = std::atoi(bl);
     if (const char* bw2 = std::getenv("FFDDP_BW_W2_MAX")) h->bw_w2_max = std::atoi(bw2);

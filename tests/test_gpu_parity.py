@@ -369,18 +369,14 @@ def test_gravity_torque_dev_matches_oracle():
 
 
 # Every launch setting the library reads (include/INTEGRATION.md §4): at
-# B = 520 (one slice by default, 4 slices of 130 or 8 of 65 under
-# FFDDP_STREAMS) each setting gives, bit for bit, the
+# B = 520 (4 slices of 130, or 8 of 65) each setting gives, bit for bit, the
 # default schedule's solution -- the per-instance arithmetic does not depend
 # on slicing, stream placement, stagger, line-search pass split or backward
 # variant (the default schedule is itself checked against the oracle at
 # B = 4096 / 517 in tests/test_gpu_batch.py).
-# (B = 520 runs as one slice by default: the stagger / caller-slice settings
-# are checked with FFDDP_STREAMS=4)
 ENV_VARIANTS = [
-    {"FFDDP_FW_SCHED": "1,3,5"}, {"FFDDP_FW_SCHED": "10"}, {"FFDDP_FW_FIRST": "1"}, {"FFDDP_STREAMS": "4"},
-    {"FFDDP_STREAMS": "4", "FFDDP_STAGGER": "0"}, {"FFDDP_STREAMS": "4", "FFDDP_STAGGER": "1"},
-    {"FFDDP_STREAMS": "4", "FFDDP_STAGGER": "2"}, {"FFDDP_STREAMS": "4", "FFDDP_CALLER_SLICE": "0"},
+    {"FFDDP_FW_SCHED": "1,3,5"}, {"FFDDP_FW_SCHED": "10"}, {"FFDDP_FW_FIRST": "1"}, {"FFDDP_STREAMS": "1"},
+    {"FFDDP_STAGGER": "0"}, {"FFDDP_STAGGER": "1"}, {"FFDDP_STAGGER": "2"}, {"FFDDP_CALLER_SLICE": "0"},
     {"FFDDP_STREAMS": "2"}, {"FFDDP_STREAMS": "3"}, {"FFDDP_STREAMS": "8"}, {"FFDDP_BW_LATE_MAX": "0"},
     {"FFDDP_BW_LATE_MAX": "100000"}, {"FFDDP_FW_FILL": "0"},
     {"FFDDP_BW_W2_MAX": "0"}, {"FFDDP_BW_W2_MAX": "100000"},
