@@ -355,12 +355,14 @@ def main():
         for key, hs, inp in (("pageable", solver, mine), ("pinned_outputs", pinned, mine),
                              ("pinned", pinned, pin_in)):
             hs.solve(inp, maxiter=args.maxiter)
-            th0 = time.perf_counter()
-            reps = 5
-            for _ in range(reps):
+            # median of 9 timed calls (single calls vary with host-side jitter)
+            ts = []
+            for _ in range(9):
+                th0 = time.perf_counter()
                 hs.solve(inp, maxiter=args.maxiter)
-            th = (time.perf_counter() - th0) / reps
-            host_io[key] = {"value": mine.B / th, "ms_per_step": th * 1e3}
+                ts.append(time.perf_counter() - th0)
+            th = float(np.median(ts))
+            host_io[key] = {"value": mine.B / th, "ms_per_step": th * 1e3, "reps": len(ts)}
         assert np.array_equal(pinned.xs, solver.xs) and np.array_equal(pinned.K, solver.K)
         pinned.close()
         del pin_in
