@@ -1565,7 +1565,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
     TrialRes T;
     load_trials(d, b, tr0, T);
     bool any = false;
-    for (int t2 = 0; t2 < tr0 && !any; ++t2) any = trial_accepted(C, sv, T, t2);
+    // constant trip count: T stays in registers (a runtime bound indexes
+    // it dynamically, i.e. through scratch memory)
+#pragma unroll
+    for (int t2 = 0; t2 < NTRIALS; ++t2) any = any || (t2 < tr0 && trial_accepted(C, sv, T, t2));
     if (any) return;
   }
 #ifdef FFDDP_PHASE_PROF
