@@ -1,3 +1,5 @@
+"""Raw kernel-trace listing around the start of the last solve in a rocprofv3
+kernel trace (every dispatch, all queues).  usage: rawtl.py <trace dir>"""
 import csv,glob,sys
 f=glob.glob(sys.argv[1]+"/**/*kernel_trace.csv",recursive=True)[0]
 rows=list(csv.DictReader(open(f)))
