@@ -687,6 +687,7 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
     const double dx = cl ? 0.0 : xsf - x;
     if (lane0(max8(fabs(dx)) < C.qp_th_grad)) break;
     const double fold = g8_sum(0.5 * x * hx + q * x);
+    bool moved = false;
 #pragma unroll 1
     for (int ia = 0; ia < NTRIALS; ++ia) {
       const double al = C.alphas[ia];
@@ -698,9 +699,17 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
       const double gd = g8_sum(g * (x - xn));
       if (lane0(fold - fnew > C.qp_th_acceptstep * gd)) {
         x = xn;
+        moved = true;
         break;
       }
     }
+    // No step length accepted: x is unchanged, so every remaining iteration
+    // recomputes the same gradient, clamped set and direction and rejects the
+    // same trials (BoxQP::solve runs them to maxiter).  Stopping here returns
+    // exactly what the remaining iterations would.  On the random-x0 workload
+    // ~1 QP in 1600 stagnates this way, and its ~90 repeated iterations
+    // (10 trials each) set the backward launch's tail.
+    if (!moved) break;
   }
   return true;
 }

@@ -25,7 +25,7 @@ from ffddp import BatchedBoxFDDP
 from helpers import make_batch, product_cfg
 
 out = {}
-for variant, B, regime in (("classical", 512, "tracking"), ("classical", 256, "random"), ("ff", 256, "tracking")):
+for variant, B, regime in (("classical", 512, "tracking"), ("classical", 1024, "random"), ("ff", 256, "tracking")):
     cfg = product_cfg(variant, 30)
     b = make_batch(variant, B, 30, seed=91, regime=regime)
     s = BatchedBoxFDDP(cfg, max_batch=B)
