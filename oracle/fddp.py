@@ -93,12 +93,21 @@ def llt_solve(L, B):
     return X if B.ndim == 2 else X[:, 0]
 
 
-def boxqp(H, q, lb, ub, xinit, c: Consts):
-    """crocoddyl::BoxQP::solve (projected Newton).  Returns x, free, clamped, Hff_inv."""
+def boxqp(H, q, lb, ub, xinit, c: Consts, stall_exit: bool = False, info: dict | None = None):
+    """crocoddyl::BoxQP::solve (projected Newton).  Returns x, free, clamped, Hff_inv.
+
+    stall_exit: stop at the first iteration whose line search accepts no step
+    length (the kernel's rule, boxqp_lanes); Crocoddyl runs on to maxiter with
+    x unchanged.  info (optional dict) receives the iterations run and whether
+    the loop stopped that way."""
     n = q.shape[0]
     x = np.maximum(np.minimum(xinit, ub), lb)
     free, clamped, Hff_inv = list(range(n)), [], None
+    if info is not None:
+        info.update(iters=0, stalled=False)
     for _ in range(c.qp_maxiter):
+        if info is not None:
+            info["iters"] += 1
         g = q + H @ x
         free, clamped = [], []
         for j in range(n):
@@ -127,6 +136,13 @@ def boxqp(H, q, lb, ub, xinit, c: Consts):
             fnew = 0.5 * xn @ (H @ xn) + q @ xn
             if fold - fnew > c.qp_th_acceptstep * (g @ (x - xn)):
                 x = xn
+                break
+        else:
+            if info is not None and not info["stalled"]:
+                info["stall_iter"] = info["iters"] - 1
+            if info is not None:
+                info["stalled"] = True
+            if stall_exit:
                 break
     return x, free, clamped, Hff_inv
 

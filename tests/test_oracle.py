@@ -276,6 +276,24 @@ def test_boxqp_matches_bruteforce(seed):
         assert np.allclose(Hinv, np.linalg.inv(H[np.ix_(free, free)]), atol=1e-10)
 
 
+def test_boxqp_stagnation_exit():
+    """The kernel's BoxQP (boxqp_lanes) stops at the first projected-Newton
+    iteration whose line search accepts no step length; crocoddyl::BoxQP::solve
+    runs on to maxiter with x unchanged.  On a QP from the random-x0 batch
+    where this happens (tests/golden/make_boxqp_stagnation.py), stopping there
+    returns exactly what the full 100 iterations return."""
+    g = np.load(Path(__file__).parent / "golden" / "boxqp_stagnation.npz")
+    args = (g["H"], g["q"], g["lb"], g["ub"], g["xinit"], fddp.Consts())
+    i_full, i_stop = {}, {}
+    full = fddp.boxqp(*args, info=i_full)
+    stop = fddp.boxqp(*args, stall_exit=True, info=i_stop)
+    assert i_full["stalled"] and i_full["iters"] == fddp.Consts().qp_maxiter
+    assert i_stop["iters"] == i_full["stall_iter"] + 1 == int(g["stall_iter"]) + 1 < 10
+    assert np.array_equal(full[0], stop[0])
+    assert full[1] == stop[1] and full[2] == stop[2]
+    assert np.array_equal(full[3], stop[3])
+
+
 def test_backward_failure_raises_regularisation():
     """A non-convex Luu makes the first LLT fail: preg grows (SolverFDDP retry)."""
     rng = np.random.default_rng(6)
