@@ -1539,6 +1539,16 @@ __device__ __forceinline__ bool trial_accepted(const DevConsts& C, const InstSta
                                                : dV > C.th_acceptnegstep * dVexp;
 }
 
+// Width of the line search's first pass, decided on the device from the
+// slice's active count: every step length at once while the active instances
+// fit the threshold wide_max (then the second pass, a whole extra rollout on
+// the iteration's chain, never runs), else the host's width n1.  The first
+// pass, the second pass and k_accept all read the same active count.  Which
+// trials run in which pass changes no result (each trial is evaluated alone).
+__device__ __forceinline__ int first_width(int n1, int n_act, int wide_max) {
+  return n_act <= wide_max ? NTRIALS : n1;
+}
+
 // one wave per SIMD: the register budget holds the next node's K row,
 // prefetched one node ahead (a 2-waves/SIMD variant without the prefetch
 // measured slower in every iteration)
@@ -1548,10 +1558,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
                                                    const double* __restrict__ node_ref,
                                                    const double* __restrict__ inst_ref,
                                                    const uint8_t* __restrict__ surface, int tr0, int ntr,
-                                                   int only_more, int cur) {
+                                                   int only_more, int cur, int wide_max) {
   const DevConsts& C = *Cg;
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
+  // host: first pass (0, n1), second pass (n1, NTRIALS - n1); the device may
+  // widen the first pass to all step lengths (first_width)
+  {
+    const int n1 = first_width(only_more ? tr0 : ntr, d.acnt[cur], wide_max);
+    tr0 = only_more ? n1 : 0;
+    ntr = only_more ? NTRIALS - n1 : n1;
+    if (ntr == 0) return;
+  }
   const long blk = xcd_block(blockIdx.x, ((long)d.acnt[cur] * ntr * G8 + 63) / 64);
   const long gid = (blk * (long)blockDim.x + threadIdx.x) / G8;
   const int li = g8_lane();
@@ -1806,9 +1824,11 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int 
 // per wave.  The accepted trial is not copied here: the next iteration's
 // k_node reads it in place and writes it into (xs, us) node by node, and
 // k_commit does it for the instances no further k_node visits.
-__global__ __launch_bounds__(64) void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1, int cur) {
+__global__ __launch_bounds__(64) void k_accept(const DevConsts* __restrict__ Cg, Dev d, int iter, int n1, int cur,
+                                               int wide_max) {
   const DevConsts& C = *Cg;
   const ActiveList al = active_list(d, cur);
+  n1 = first_width(n1, al.n, wide_max);
   if ((int)blockIdx.x * 64 >= al.n) return;
   const int slot = (int)blockIdx.x * 64 + (int)threadIdx.x;
   const bool has = slot < al.n;
@@ -2104,6 +2124,8 @@ struct ffddp_handle {
   int bw_w2_max = -1;    // ... and the two-wave variant (FFDDP_BW_W2_MAX; -1: SIMDs / (2 slices); 0: never)
   int n_simd = 1024;     // SIMDs of the device (4 per CU)
   bool fw_fill = true;   // widen the first line-search pass to fill the SIMDs (FFDDP_FW_FILL=0: off)
+  int fw_wide_max = -1;  // active instances per slice up to which the first pass takes every step length
+                         // (decided on the device; FFDDP_FW_WIDE_MAX; -1: SIMDs / slices; 0: never)
   // optional per-kernel timing
   bool prof = false;
   int prof_mask = 0;
@@ -2320,10 +2342,17 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
         // B=1024: +4.5 %; at N=30 the two extra trials cost more than the
         // rare second pass saves)
         if (h->fw_fill && N >= 60 && n1 >= 8) n1 = NTRIALS;
+        // device-side widening of the first pass: while a slice's active
+        // instances fit one wave per SIMD share at every step length, all ten
+        // run at once (random x0 at B=1024: the second pass ran in every
+        // iteration)
+        const int wide = h->fw_wide_max >= 0 ? h->fw_wide_max : h->n_simd / S;
+        const long g1 = std::max((long)Bk * n1, (long)std::min(Bk, wide) * NTRIALS);  // first-pass groups
         auto fw = [&](int tr0, int ntr, int more) {
-          const dim3 grid((unsigned)(((long)Bk * ntr * G8 + 63) / 64));
+          const long groups = more ? (long)Bk * ntr : g1;
+          const dim3 grid((unsigned)((groups * G8 + 63) / 64));
           hipLaunchKernelGGL((k_forward_g8<NC, FF>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk, tr0,
-                             ntr, more, it & 1);
+                             ntr, more, it & 1, wide);
         };
         {
           ProfScope p(h, ss, KC_FORWARD);
@@ -2336,7 +2365,8 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       }
       {
         ProfScope p(h, ss, KC_ACCEPT);
-        hipLaunchKernelGGL(k_accept, dim3((Bk + 63) / 64), dim3(64), 0, ss, h->dc, d, it, n1, it & 1);
+        hipLaunchKernelGGL(k_accept, dim3((Bk + 63) / 64), dim3(64), 0, ss, h->dc, d, it, n1, it & 1,
+                           h->fw_wide_max >= 0 ? h->fw_wide_max : h->n_simd / S);
       }
     }
   }
@@ -2524,6 +2554,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     if (const char* bl = std::getenv("FFDDP_BW_LATE_MAX")) h->bw_late_max = std::atoi(bl);
     if (const char* bw2 = std::getenv("FFDDP_BW_W2_MAX")) h->bw_w2_max = std::atoi(bw2);
     if (const char* ff = std::getenv("FFDDP_FW_FILL")) h->fw_fill = std::atoi(ff) != 0;
+    if (const char* fwm = std::getenv("FFDDP_FW_WIDE_MAX")) h->fw_wide_max = std::atoi(fwm);
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
       h->fw_sched.clear();
       for (const char* p = fsch; *p;) {

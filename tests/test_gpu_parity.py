@@ -378,7 +378,10 @@ ENV_VARIANTS = [
     {"FFDDP_FW_SCHED": "1,3,5"}, {"FFDDP_FW_SCHED": "10"}, {"FFDDP_FW_FIRST": "1"}, {"FFDDP_STREAMS": "1"},
     {"FFDDP_STAGGER": "0"}, {"FFDDP_STAGGER": "1"}, {"FFDDP_STAGGER": "2"}, {"FFDDP_CALLER_SLICE": "0"},
     {"FFDDP_STREAMS": "2"}, {"FFDDP_STREAMS": "3"}, {"FFDDP_STREAMS": "8"}, {"FFDDP_BW_LATE_MAX": "0"},
-    {"FFDDP_BW_LATE_MAX": "100000"}, {"FFDDP_FW_FILL": "0"},
+    {"FFDDP_BW_LATE_MAX": "100000"}, {"FFDDP_FW_FILL": "0", "FFDDP_FW_WIDE_MAX": "0"},
+    # device-side first-pass width: two passes while a slice has > 60 active
+    # instances, all ten step lengths in one pass below
+    {"FFDDP_FW_FILL": "0", "FFDDP_FW_WIDE_MAX": "60"}, {"FFDDP_FW_FILL": "0"},
     {"FFDDP_BW_W2_MAX": "0"}, {"FFDDP_BW_W2_MAX": "100000"},
 ]
 
@@ -409,9 +412,12 @@ def test_launch_settings_bit_identical(variant, monkeypatch):
 # Launch-schedule variants (the small parity batches otherwise always take
 # the latency variant of the backward pass and a single 10-step-length line
 # search pass): the same solves through the 2-waves/SIMD backward variant and
-# through the two-pass line search (2 step lengths first, the rest second).
-@pytest.mark.parametrize("env", [{"FFDDP_BW_LATE_MAX": "0"}, {"FFDDP_BW_W2_MAX": "0"}, {"FFDDP_FW_FILL": "0"},
-                                 {"FFDDP_BW_LATE_MAX": "0", "FFDDP_FW_FILL": "0", "FFDDP_FW_FIRST": "2"}])
+# through the two-pass line search (2 step lengths first, the rest second;
+# FFDDP_FW_WIDE_MAX=0 keeps the device from widening the first pass).
+@pytest.mark.parametrize("env", [{"FFDDP_BW_LATE_MAX": "0"}, {"FFDDP_BW_W2_MAX": "0"},
+                                 {"FFDDP_FW_FILL": "0", "FFDDP_FW_WIDE_MAX": "0"},
+                                 {"FFDDP_BW_LATE_MAX": "0", "FFDDP_FW_FILL": "0", "FFDDP_FW_WIDE_MAX": "0",
+                                  "FFDDP_FW_FIRST": "2"}])
 @pytest.mark.parametrize("variant", ["classical", "ff"])
 def test_solve_schedule_variants(variant, env, monkeypatch):
     for k, v in env.items():

@@ -2,7 +2,8 @@
 how many step lengths each still-active instance tried (1 = alpha 1 accepted,
 ..., 10 with none accepted).  Solves with maxiter = 1..10 replay the same
 deterministic iterations; the difference of the device-counted trials gives
-iteration k's count.  usage: python tools/accept_hist.py [B] [variant]"""
+iteration k's count.  usage: python tools/accept_hist.py [B] [variant] [save.npy]
+(REGIME=random for the random-x0 draw)"""
 import sys
 import pathlib
 
@@ -18,7 +19,8 @@ variant = sys.argv[2] if len(sys.argv) > 2 else "classical"
 N = 30
 cfg = ff_preset(N) if variant == "ff" else classical_preset(N)
 ee = R.R_MJ_FROM_PIN @ _abi.frame_placement(R.Q_NEUTRAL)[1]
-b = workload.make_batch(B, N, variant, _abi.gravity_torque, ee, seed=1234, fk=_abi.frame_placement)
+b = workload.make_batch(B, N, variant, _abi.gravity_torque, ee, seed=1234, fk=_abi.frame_placement,
+                        regime=__import__("os").environ.get("REGIME", "tracking"))
 s = BatchedBoxFDDP(cfg, max_batch=B)
 prev_tr = np.zeros(B, np.int64)
 hist = np.zeros((10, B), np.int64)  # per-instance tried count per iteration (0: did not run)
