@@ -83,7 +83,8 @@ struct Dev {
   int* trial_fail;   // [B][T]
   InstState* st;     // [B]
   int* alist;        // [2][B]  active-instance lists (slice-local indices), double-buffered over iterations
-  int* acnt;         // [2]     their lengths
+  int* acnt;         // [4]     their lengths; [2 + p]: an instance of the iteration that built list p
+                     //         needed more step lengths than the host's first pass (first_width)
   double* trace;     // [B][trace_it][FFDDP_TRACE_W] per-iteration records (CallbackVerbose), or null
   int trace_it;
 };
@@ -143,6 +144,8 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
       if (i == 0) {
         d.acnt[0] = d.B;
         d.acnt[1] = 0;
+        d.acnt[2] = 0;
+        d.acnt[3] = 0;
       }
       InstState s;
       s.preg = C.reg_min;
@@ -728,7 +731,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   const DevConsts& C = *Cg;
   const int N = C.N;
   const int l = threadIdx.x;
-  if (blockIdx.x == 0 && l == 0) d.acnt[cur ^ 1] = 0;  // the list k_accept builds
+  if (blockIdx.x == 0 && l == 0) d.acnt[cur ^ 1] = d.acnt[2 + (cur ^ 1)] = 0;  // the list k_accept builds
   const ActiveList al = active_list(d, cur);
   // active-count ranges: (late_max, B] this variant, (w2_max, late_max] LATE,
   // [1, w2_max] the two-wave k_backward_w2
@@ -1113,7 +1116,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
   const int N = C.N;
   const int tid = threadIdx.x;
   const int wv = tid >> 6, l = tid & 63;
-  if (blockIdx.x == 0 && tid == 0) d.acnt[cur ^ 1] = 0;  // the list k_accept builds
+  if (blockIdx.x == 0 && tid == 0) d.acnt[cur ^ 1] = d.acnt[2 + (cur ^ 1)] = 0;  // the list k_accept builds
   const ActiveList al = active_list(d, cur);
   if ((int)blockIdx.x >= al.n || al.n > w2_max) return;
   const int b = al.list[blockIdx.x];
@@ -1539,14 +1542,15 @@ __device__ __forceinline__ bool trial_accepted(const DevConsts& C, const InstSta
                                                : dV > C.th_acceptnegstep * dVexp;
 }
 
-// Width of the line search's first pass, decided on the device from the
-// slice's active count: every step length at once while the active instances
-// fit the threshold wide_max (then the second pass, a whole extra rollout on
-// the iteration's chain, never runs), else the host's width n1.  The first
-// pass, the second pass and k_accept all read the same active count.  Which
-// trials run in which pass changes no result (each trial is evaluated alone).
-__device__ __forceinline__ int first_width(int n1, int n_act, int wide_max) {
-  return n_act <= wide_max ? NTRIALS : n1;
+// Width of the line search's first pass, decided on the device: every step
+// length at once while the slice's active instances fit the threshold
+// wide_max and the previous iteration had an instance that needed more than
+// the host's width n1 (then the second pass, a whole extra rollout on the
+// iteration's chain, would likely run again), else n1.  The first pass, the
+// second pass and k_accept read the same two values.  Which trials run in
+// which pass changes no result (each trial is evaluated alone).
+__device__ __forceinline__ int first_width(int n1, const Dev& d, int cur, int wide_max) {
+  return (d.acnt[cur] <= wide_max && d.acnt[2 + cur] != 0) ? NTRIALS : n1;
 }
 
 // one wave per SIMD: the register budget holds the next node's K row,
@@ -1565,7 +1569,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
   // host: first pass (0, n1), second pass (n1, NTRIALS - n1); the device may
   // widen the first pass to all step lengths (first_width)
   {
-    const int n1 = first_width(only_more ? tr0 : ntr, d.acnt[cur], wide_max);
+    const int n1 = first_width(only_more ? tr0 : ntr, d, cur, wide_max);
     tr0 = only_more ? n1 : 0;
     ntr = only_more ? NTRIALS - n1 : n1;
     if (ntr == 0) return;
@@ -1828,16 +1832,21 @@ __global__ __launch_bounds__(64) void k_accept(const DevConsts* __restrict__ Cg,
                                                int wide_max) {
   const DevConsts& C = *Cg;
   const ActiveList al = active_list(d, cur);
-  n1 = first_width(n1, al.n, wide_max);
+  const int n1h = n1;
+  n1 = first_width(n1, d, cur, wide_max);
   if ((int)blockIdx.x * 64 >= al.n) return;
   const int slot = (int)blockIdx.x * 64 + (int)threadIdx.x;
   const bool has = slot < al.n;
   const int b = has ? al.list[slot] : 0;
   bool cont = false;
+  int acc = -1;
   if (has) {
-    accept_instance(C, d, b, iter, n1);
+    acc = accept_instance(C, d, b, iter, n1);
     cont = d.st[b].done == 0;
   }
+  // a continuing instance needed more step lengths than the host's first pass:
+  // the next iteration's first pass may take them all (first_width)
+  if (cont && (acc < 0 || acc >= n1h)) d.acnt[2 + (cur ^ 1)] = 1;
   const unsigned long long m = __ballot(cont);
   int base = 0;
   if (threadIdx.x == 0 && m != 0ull) base = atomicAdd(d.acnt + (cur ^ 1), __popcll(m));
@@ -2219,7 +2228,7 @@ Dev dev_slice(const Dev& d0, int b0, int Bk, int k) {
   d.trial_fail += (long)b0 * NTRIALS;
   d.st += b0;
   d.alist += 2L * b0;
-  d.acnt += 2 * k;
+  d.acnt += 4 * k;
   if (d.trace) d.trace += (long)b0 * d0.trace_it * FFDDP_TRACE_W;
   return d;
 }
@@ -2588,7 +2597,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   rc |= dalloc(h, &d.trial_fail, (size_t)B * NTRIALS);
   rc |= dalloc(h, &d.st, (size_t)B);
   rc |= dalloc(h, &d.alist, (size_t)B * 2);
-  rc |= dalloc(h, &d.acnt, (size_t)2 * 8);
+  rc |= dalloc(h, &d.acnt, (size_t)4 * 8);
   rc |= dalloc(h, &h->in_x0, (size_t)B * nx);
   rc |= dalloc(h, &h->in_nref, (size_t)B * (N + 1) * 6);
   rc |= dalloc(h, &h->in_iref, (size_t)B * 21);
