@@ -335,17 +335,26 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
   if (active && lane < G8) primal_group<NC, FF>(C, d, x0, node_ref, inst_ref, surface, b, t, &P, G.lk, xsrc, usrc);
   __syncthreads();
   const bool need_u = mode != MODE_TERMINAL_X;
-  double da[NQ], dlam[3], col[NDENSE_MAX];
-  double dau[NQ], dlamu[3];
-  if (active && lane < 14) {
-    node_tangent_state_an<NC>(C, mode, surf, G.lk, P, lane, da, dlam, col);
-  }
-  if (active && lane < 7 && need_u) node_tangent_control<NC>(C, surf, P, lane, dau, dlamu);
-  __syncthreads();  // every lane's reads of lk are done before col overwrites it
-  if (active && lane < 14)
-    for (int r = 0; r < 12 + nc; ++r) G.col[lane][r] = col[r];
-  if (active && lane < 7 && need_u)
+  // control directions first, their results stored at once (neither touches
+  // lk), so they are not live across the state tangent: no scratch spill at
+  // 2 waves/SIMD
+  if (active && lane < 7 && need_u) {
+    double dau[NQ], dlamu[3];
+    node_tangent_control<NC>(C, surf, P, lane, dau, dlamu);
+    double* rec = d.rec_buf + ((long)b * (N + 1) + t) * d.rec;
+    for (int i = 0; i < NQ; ++i) rec[rec_off_A() + (14 + lane) * NQ + i] = dau[i];
     for (int r = 0; r < nc; ++r) G.colu[lane][r] = (surf ? dlamu[r] : 0.0);
+  }
+  double da[NQ], dlam[3], col[NDENSE_MAX], r1[NQ], dh[3];
+  if (active && lane < 14) node_tangent_state_links<NC>(C, mode, surf, G.lk, P, lane, r1, dh, col);
+  __syncthreads();  // every lane's reads of lk are done before col overwrites it
+  // the column's rows 0..11 go to LDS before the contact solves (which read
+  // only P), so they are not live across them: no scratch spill at 2 waves/SIMD
+  if (active && lane < 14) {
+    for (int r = 0; r < 12; ++r) G.col[lane][r] = col[r];
+    node_tangent_state_contact<NC>(mode, surf, P, r1, dh, da, dlam, col);
+    for (int r = 12; r < 12 + nc; ++r) G.col[lane][r] = col[r];
+  }
   __syncthreads();
   if (active) {
     double* rec = d.rec_buf + ((long)b * (N + 1) + t) * d.rec;
@@ -391,7 +400,6 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
     }
     if (lane < 7 && need_u) {
       const int kk = lane;
-      for (int i = 0; i < NQ; ++i) rec[rec_off_A() + (14 + kk) * NQ + i] = dau[i];
       // Luu_in column kk
       double luu[7];
       for (int m = 0; m < NU; ++m) {

@@ -656,9 +656,14 @@ FFD_HD void sp_imul(double m, const double* h, const double* IO, const double* x
   on[2] = (h[0] * xv[1] - h[1] * xv[0]) + IO[2] * xw[0] + IO[4] * xw[1] + IO[5] * xw[2];
 }
 
+// Two parts, so a kernel can store the residual-Jacobian column between them
+// (k_node: the column is not live across the contact solves):
+//   node_tangent_state_links    link-record part: the column (force rows 0),
+//                               d tau (r1) and dh; reads LK and P
+//   node_tangent_state_contact  contact solves: da, dlam, force rows; reads P only
 template <int NC>
-FFD_HD void node_tangent_state_an(const DevConsts& C, int mode, bool surface, const double* LK, const Primal& P,
-                                  int dir, double* da, double* dlam, double* col) {
+FFD_HD void node_tangent_state_links(const DevConsts& C, int mode, bool surface, const double* LK, const Primal& P,
+                                     int dir, double* r1, double* dh, double* col) {
   constexpr int nc = NC;
   const bool with_dyn = mode != MODE_TERMINAL_X;
   const bool isq = dir < NQ;
@@ -757,6 +762,12 @@ FFD_HD void node_tangent_state_an(const DevConsts& C, int mode, bool surface, co
 #pragma unroll
     for (int k = 0; k < 3; ++k) dap[k] = dA6v[k] + c3[k] + c4[k] + c5[k] + c6[k];
   }
+  // dh = d (classical acc + Kp (p - p*) + Kd v_p) / d x_j
+  {
+    constexpr int c0 = NC == 1 ? 2 : 0;
+#pragma unroll
+    for (int r = 0; r < nc; ++r) dh[r] = dap[c0 + r] + C.Kp * dpee[c0 + r] + C.Kd * dvp[c0 + r];
+  }
   // ---- residual-Jacobian column ----
   {
     double wl[3];
@@ -778,8 +789,7 @@ FFD_HD void node_tangent_state_an(const DevConsts& C, int mode, bool surface, co
     for (int r = 0; r < nc; ++r) col[12 + r] = 0.0;
   }
 #pragma unroll
-  for (int i = 0; i < NQ; ++i) da[i] = 0.0;
-  dlam[0] = dlam[1] = dlam[2] = 0.0;
+  for (int i = 0; i < NQ; ++i) r1[i] = 0.0;
   if (!with_dyn) return;
   // ---- d tau = d RNEA(q, v, a, fext = lambda) / d x_j at fixed a, lambda ----
   double lw[3] = {0, 0, 0};
@@ -792,7 +802,6 @@ FFD_HD void node_tangent_state_an(const DevConsts& C, int mode, bool surface, co
   dFe[1] = dpee[2] * lw[0] - dpee[0] * lw[2];
   dFe[2] = dpee[0] * lw[1] - dpee[1] * lw[0];
   double FSf[3] = {0, 0, 0}, FSn[3] = {0, 0, 0}, dSf[3] = {0, 0, 0}, dSn[3] = {0, 0, 0};
-  double r1[NQ];
 #pragma unroll
   for (int k = NQ - 1; k >= 0; --k) {
     const double* Lk = LK + k * LK_STRIDE;
@@ -853,17 +862,24 @@ FFD_HD void node_tangent_state_an(const DevConsts& C, int mode, bool surface, co
                          Szk[2] * dFtn[2]);
     r1[k] = -dtau;
   }
-  if (!surface) {
-    chol_solve<NQ>(P.L, r1);
+}
+
+template <int NC>
+FFD_HD void node_tangent_state_contact(int mode, bool surface, const Primal& P, const double* r1, const double* dh,
+                                       double* da, double* dlam, double* col) {
+  constexpr int nc = NC;
+  dlam[0] = dlam[1] = dlam[2] = 0.0;
+  if (mode == MODE_TERMINAL_X) {
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) da[i] = r1[i];
+    for (int i = 0; i < NQ; ++i) da[i] = 0.0;
     return;
   }
-  // dh = d (classical acc + Kp (p - p*) + Kd v_p) / d x_j
-  constexpr int c0 = NC == 1 ? 2 : 0;
-  double dh[3];
+  if (!surface) {
 #pragma unroll
-  for (int r = 0; r < nc; ++r) dh[r] = dap[c0 + r] + C.Kp * dpee[c0 + r] + C.Kd * dvp[c0 + r];
+    for (int i = 0; i < NQ; ++i) da[i] = r1[i];
+    chol_solve<NQ>(P.L, da);
+    return;
+  }
   double mr[NQ];
 #pragma unroll
   for (int i = 0; i < NQ; ++i) mr[i] = r1[i];
@@ -888,8 +904,17 @@ FFD_HD void node_tangent_state_an(const DevConsts& C, int mode, bool surface, co
 #pragma unroll
   for (int r = 0; r < nc; ++r) {
     dlam[r] = -yl[r];
-    col[12 + r] = (mode == MODE_TERMINAL_X) ? 0.0 : dlam[r];
+    col[12 + r] = dlam[r];
   }
+}
+
+// da = d a / d x_dir, dlam, residual-Jacobian column dir (both parts)
+template <int NC>
+FFD_HD void node_tangent_state_an(const DevConsts& C, int mode, bool surface, const double* LK, const Primal& P,
+                                  int dir, double* da, double* dlam, double* col) {
+  double r1[NQ], dh[3];
+  node_tangent_state_links<NC>(C, mode, surface, LK, P, dir, r1, dh, col);
+  node_tangent_state_contact<NC>(mode, surface, P, r1, dh, da, dlam, col);
 }
 
 // control direction k in [0,7): dg = -e_k, dh = 0
