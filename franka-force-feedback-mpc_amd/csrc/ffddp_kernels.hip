@@ -520,6 +520,8 @@ template <bool FF> struct BwW {
   double K[NU * NX];
   double H[NU * NU];  // Quu + preg I (contiguous copy for the gains lane)
   double L[28];       // packed (masked) Cholesky factor, reciprocal diagonal
+  double L1[28];      // k_backward_w2: wave 1's factor of the full set (speculative gains)
+  int spec;           // k_backward_w2: wave 1's K (and LLT k) from L1 are valid
   double Vx[NX], Qv[ND], kk[NU], z[NU];
   double fs[64], kp[64], uu[64], ulb[64], uub[64];  // one slot per lane: written without lane guards
   int flag;
@@ -1351,13 +1353,60 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
           for (int j = 0; j < NU; ++j)
             if (j <= l) S.L[tri(l, j)] = Lr[j];
         if (l == 0) S.flag = ok ? 1 : 0;
-      } else if (t > 0) {
+      } else {
+        if (t > 0) {
 #pragma unroll
-        for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
-        const int tn = t > 1 ? t - 2 : 0;
-        const double* r1 = recb + (long)tn * REC;
+          for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
+          const int tn = t > 1 ? t - 2 : 0;
+          const double* r1 = recb + (long)tn * REC;
 #pragma unroll
-        for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
+          for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
+        }
+        // Speculative gains on wave 1: the factor of the full set (Quu, or
+        // Quu + qp_reg I as BoxQP factors an empty clamped set: the same
+        // operations, so the same bits) and phase E's K columns (and the LLT
+        // k) from it, while wave 0 runs the gains.  Used when the final
+        // clamped set is empty (always for LLT); otherwise phase E runs.
+        double hrow[NU], Lr[NU];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.H[l * NU + j] : (l == j ? 1.0 : 0.0);
+#pragma unroll
+        for (int j = 0; j < NU; ++j) Lr[j] = use_qp ? hrow[j] + (l == j ? C.qp_reg : 0.0) : hrow[j];
+        const bool ok1 = chol_rows(Lr, l);
+        if (ok1) {
+          if (l < NU)
+#pragma unroll
+            for (int j = 0; j < NU; ++j)
+              if (j <= l) S.L1[tri(l, j)] = Lr[j];
+          // lanes of this wave read the rows the others just wrote: LDS
+          // accesses of one wave complete in order; the fence keeps the
+          // compiler from moving the reads above the writes
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+          if (l < NX || (!use_qp && l == NX)) {
+            double col[NU];
+            if (l < NX) {
+#pragma unroll
+              for (int c = 0; c < NU; ++c) col[c] = S.Q[l * ND + NX + c];
+            } else {
+#pragma unroll
+              for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
+            }
+            chol_solve<NU>(S.L1, col);
+            if (l < NX) {
+              double* Kt = d.K + ((long)b * N + t) * NU * NX;
+#pragma unroll
+              for (int c = 0; c < NU; ++c) {
+                S.K[c * NX + l] = col[c];
+                Kt[c * NX + l] = col[c];
+              }
+            } else {
+#pragma unroll
+              for (int c = 0; c < NU; ++c) S.kk[c] = col[c];
+            }
+          }
+        }
+        if (l == 0) S.spec = ok1 ? 1 : 0;
       }
       lds_sync();
       PP(4);
@@ -1365,8 +1414,14 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
         failed = true;
         break;
       }
+      // wave 1's gains stand unless BoxQP clamped a control
+      bool spec_ok = S.spec != 0;
+      if (use_qp) {
+#pragma unroll
+        for (int c = 0; c < NU; ++c) spec_ok = spec_ok && S.clamped[c] == 0;
+      }
       // ---- phase E: K columns (and k for LLT), wave 0 ----
-      if (wv == 0 && (l < NX || (!use_qp && l == NX))) {
+      if (!spec_ok && wv == 0 && (l < NX || (!use_qp && l == NX))) {
         double col[NU];
         if (l < NX) {
 #pragma unroll
@@ -1388,7 +1443,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
           for (int c = 0; c < NU; ++c) S.kk[c] = col[c];
         }
       }
-      lds_sync();
+      if (!spec_ok) lds_sync();  // (uniform: read from LDS)
       PP(5);
       // ---- phase F: Vxx = sym(Qxx - Qxu K) + preg I, entries over 128 lanes ----
       int badv = 0;
