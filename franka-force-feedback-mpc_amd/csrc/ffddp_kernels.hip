@@ -1224,9 +1224,56 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
       dq += cdq;
     }
     lds_sync();
+    // ---- phase G of node tg: Vx, gap terms, expected improvement, k (wave 0) ----
+    int badf = 0;  // wave 0's non-finite V entries of phase F, reported with its phase G
+    auto phase_g = [&](int tg) {
+      double cdg = 0.0, cdq = 0.0, cst = 0.0;
+      int badv = badf;
+      if (l < NX) {
+        double vfs = 0.0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
+        double vx = S.Qv[l];
+#pragma unroll
+        for (int c = 0; c < NU; ++c) vx -= S.K[c * NX + l] * S.Qv[NX + c];
+        if (!feas) vx += vfs;
+        badv |= bad(fabs(vx)) ? 1 : 0;
+        ffl = fmax(ffl, fabs(S.fs[l]));
+        if (!feas) {
+          d.w[((long)b * (N + 1) + tg) * NX + l] = vfs;
+          cdg -= vx * S.fs[l];
+          cdq += S.fs[l] * vfs;
+        }
+        if (l < NU) {
+          double quk = 0.0;
+#pragma unroll
+          for (int m = 0; m < NU; ++m) quk += S.H[l * NU + m] * S.kk[m];
+          const double qu = S.Qv[NX + l], kl = S.kk[l];
+          cdg += qu * kl;
+          cdq -= kl * quk;
+          cst += qu * qu;
+          d.k[((long)b * N + tg) * NU + l] = kl;
+        }
+        S.Vx[l] = vx;  // old Vx is dead after phase B
+      }
+      badv = __any(badv);
+      if (l == 0) S.badw[0] = badv;
+      // (a failed node aborts the pass, which restarts with dg / dq / stop reset)
+      dg += cdg;
+      dq += cdq;
+      stop += cst;
+    };
     for (int t = N - 1; t >= 0; --t) {
-      // ---- wave 0: this node's gap / warm start / control (record t is in LDS) ----
+      // ---- wave 0: phase G of node t+1 beside this node's phase A (one
+      // barrier less per node), then this node's gap / warm start / control
+      // (record t is in LDS) ----
       if (wv == 0) {
+        if (t < N - 1) {
+          phase_g(t + 1);
+          // z below reads Vx entries other lanes of this wave just wrote
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        }
         S.fs[l] = pfs;
         S.kp[l] = pkp;
         S.uu[l] = pus;
@@ -1252,6 +1299,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
       if (tid < NU) S.z[tid] = dt2 * S.Vx[tid] + dt * S.Vx[7 + tid];
       lds_sync();
       PP(1);
+      if (t < N - 1 && (S.badw[0] | S.badw[1])) {  // node t+1's phases F / G
+        failed = true;
+        break;
+      }
       // ---- phase B: row c of M = I~'W + 1/2 A^'Y (columns m split over the
       // two waves) ; Qv[c] = [Lx; Lu] + I~'Vx + A^'z (wave 1) ----
       if (l < ND) {
@@ -1465,51 +1516,17 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k
       if (wv == 1) {
         badv = __any(badv);
         if (l == 0) S.badw[1] = badv;
+      } else {
+        badf = badv;
       }
       lds_sync();
       PP(6);
-      // ---- phase G: Vx, gap terms, expected improvement, k (wave 0) ----
-      double cdg = 0.0, cdq = 0.0, cst = 0.0;
-      if (wv == 0) {
-        if (l < NX) {
-          double vfs = 0.0;
-#pragma unroll
-          for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
-          double vx = S.Qv[l];
-#pragma unroll
-          for (int c = 0; c < NU; ++c) vx -= S.K[c * NX + l] * S.Qv[NX + c];
-          if (!feas) vx += vfs;
-          badv |= bad(fabs(vx)) ? 1 : 0;
-          ffl = fmax(ffl, fabs(S.fs[l]));
-          if (!feas) {
-            d.w[((long)b * (N + 1) + t) * NX + l] = vfs;
-            cdg -= vx * S.fs[l];
-            cdq += S.fs[l] * vfs;
-          }
-          if (l < NU) {
-            double quk = 0.0;
-#pragma unroll
-            for (int m = 0; m < NU; ++m) quk += S.H[l * NU + m] * S.kk[m];
-            const double qu = S.Qv[NX + l], kl = S.kk[l];
-            cdg += qu * kl;
-            cdq -= kl * quk;
-            cst += qu * qu;
-            d.k[((long)b * N + t) * NU + l] = kl;
-          }
-          S.Vx[l] = vx;  // old Vx is dead after phase B
-        }
-        badv = __any(badv);
-        if (l == 0) S.badw[0] = badv;
-      }
+    }
+    if (!failed) {
+      if (wv == 0) phase_g(0);
       lds_sync();
       PP(7);
-      if (S.badw[0] | S.badw[1]) {
-        failed = true;
-        break;
-      }
-      dg += cdg;
-      dq += cdq;
-      stop += cst;
+      if (S.badw[0] | S.badw[1]) failed = true;
     }
     // ---- retry bookkeeping (SolverFDDP::solve: increaseRegularization) ----
     if (!failed) {
