@@ -2342,10 +2342,20 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
     int b0, B;
   };
   Slice sl[8];
+  // device entry point: the solve iterates in the caller's xs / us / K
+  // (same [B][N+1][nx] / [B][N][7] / [B][N][7][nx] layout as the handle's
+  // buffers), so no copy of the solution follows the last kernel; the host
+  // entry point keeps the handle's buffers (its outputs are host memory)
+  Dev dbase = h->d;
+  if (!io) {
+    dbase.xs = xs;
+    dbase.us = us;
+    dbase.K = K;
+  }
   for (int k = 0; k < S; ++k) {
     sl[k].b0 = k * Bs;
     sl[k].B = (B - sl[k].b0) < Bs ? (B - sl[k].b0) : Bs;
-    sl[k].d = dev_slice(h->d, sl[k].b0, sl[k].B, k);
+    sl[k].d = dev_slice(dbase, sl[k].b0, sl[k].B, k);
     // FFDDP_CALLER_SLICE: the last slice runs on the caller's stream (its
     // hardware queue is otherwise idle during the solve)
     sl[k].s = (S > 1 && !(h->caller_slice && k == S - 1)) ? h->streams[k] : s;
@@ -2477,12 +2487,12 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
                          x0 + b0 * nxl, nref + b0 * N1 * 6, iref + b0 * 21, surf + b0, cost + b0, iters + b0, ok + b0,
                          fn_pred ? fn_pred + 2 * b0 : nullptr, stats ? stats + b0 * FFDDP_NSTATS : nullptr);
     }
-    // device outputs (dev entry point), or page-locked host memory (host
-    // entry point: the slice's results go down as soon as it finishes)
-    HIPCHK(h, hipMemcpyAsync(xs + b0 * N1 * nxl, d.xs, bxs * Bk, hipMemcpyDefault, ss));
-    HIPCHK(h, hipMemcpyAsync(us + b0 * (long)N * NU, d.us, bus * Bk, hipMemcpyDefault, ss));
-    HIPCHK(h, hipMemcpyAsync(K + b0 * (long)N * NU * nx, d.K, bks * Bk, hipMemcpyDefault, ss));
+    // host entry point: page-locked host memory, the slice's results go
+    // down as soon as it finishes (the device entry point solved in place)
     if (io) {
+      HIPCHK(h, hipMemcpyAsync(xs + b0 * N1 * nxl, d.xs, bxs * Bk, hipMemcpyDefault, ss));
+      HIPCHK(h, hipMemcpyAsync(us + b0 * (long)N * NU, d.us, bus * Bk, hipMemcpyDefault, ss));
+      HIPCHK(h, hipMemcpyAsync(K + b0 * (long)N * NU * nx, d.K, bks * Bk, hipMemcpyDefault, ss));
       for (int i = 0; i < io->n_out; ++i) {
         const size_t o = (size_t)b0 * io->out[i].per_inst;
         HIPCHK(h, hipMemcpyAsync((char*)io->out[i].host + o, (const char*)io->out[i].dev + o,

@@ -153,7 +153,10 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
                       int32_t* stats);
 
 /* Same with DEVICE pointers (inputs resident in HBM) on `stream` (hipStream_t,
- * NULL = default stream).  Asynchronous: the caller synchronises the stream. */
+ * NULL = default stream).  Asynchronous: the caller synchronises the stream.
+ * xs / us / K are the solver's working storage during the solve (it iterates
+ * in them; no copy follows the last kernel): they must not overlap the other
+ * inputs, except xs_init == xs and us_init == us (warm start in place). */
 int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double* node_ref,
                           const double* inst_ref, const uint8_t* surface, const double* xs_init,
                           const double* us_init, int maxiter, int is_feasible, double* xs,

@@ -171,3 +171,44 @@ def test_solve_from_device_built_problem():
     assert rel_err(t["xs"].cpu().numpy(), s_host.xs) < 1e-6
     assert rel_err(t["us"].cpu().numpy(), s_host.us) < 1e-6
     assert rel_err(t["cost"].cpu().numpy(), s_host.cost) < 1e-6
+
+
+def test_solve_dev_matches_host_entry_and_in_place():
+    """The device entry point iterates in the caller's xs / us / K (no copy
+    after the last kernel): bit-identical to the host entry point at B = 520
+    (4 slices), also with the warm start in place (xs_init is xs, us_init is us)."""
+    torch = _torch()
+    N, B = 30, 520
+    b = make_batch("classical", B, N, seed=17)
+    cfg = product_cfg("classical", N)
+    s_host = BatchedBoxFDDP(cfg, max_batch=B)
+    s_host.solve(b)
+    dev = lambda a, dt=torch.float64: torch.tensor(np.ascontiguousarray(a), dtype=dt, device="cuda")
+    for in_place in (False, True):
+        s_dev = BatchedBoxFDDP(cfg, max_batch=B)
+        t = {
+            "x0": dev(b.x0), "node_ref": dev(b.node_ref), "inst_ref": dev(b.inst_ref),
+            "surface": dev(b.surface, torch.uint8),
+            "xs_init": dev(b.xs_init), "us_init": dev(b.us_init),
+            "K": torch.full((B, N, 7, 14), float("nan"), dtype=torch.float64, device="cuda"),
+            "cost": torch.empty(B, dtype=torch.float64, device="cuda"),
+            "iters": torch.empty(B, dtype=torch.int32, device="cuda"),
+            "ok": torch.empty(B, dtype=torch.uint8, device="cuda"),
+            "fn_pred": torch.empty((B, 2), dtype=torch.float64, device="cuda"),
+            "stats": torch.empty((B, _abi.NSTATS), dtype=torch.int32, device="cuda"),
+        }
+        if in_place:
+            t["xs"], t["us"] = t["xs_init"], t["us_init"]
+        else:
+            t["xs"] = torch.full((B, N + 1, 14), float("nan"), dtype=torch.float64, device="cuda")
+            t["us"] = torch.full((B, N, 7), float("nan"), dtype=torch.float64, device="cuda")
+        s_dev.solve_dev(t, maxiter=10)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(t["xs"].cpu().numpy(), s_host.xs)
+        np.testing.assert_array_equal(t["us"].cpu().numpy(), s_host.us)
+        np.testing.assert_array_equal(t["K"].cpu().numpy(), s_host.K)
+        np.testing.assert_array_equal(t["cost"].cpu().numpy(), s_host.cost)
+        np.testing.assert_array_equal(t["iters"].cpu().numpy(), s_host.iter)
+        np.testing.assert_array_equal(t["ok"].cpu().numpy().astype(bool), s_host.ok)
+        s_dev.close()
+    s_host.close()
