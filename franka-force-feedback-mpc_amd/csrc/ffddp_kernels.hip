@@ -720,8 +720,9 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
     // recomputes the same gradient, clamped set and direction and rejects the
     // same trials (BoxQP::solve runs them to maxiter).  Stopping here returns
     // exactly what the remaining iterations would.  On the random-x0 workload
-    // ~1 QP in 1600 stagnates this way, and its ~90 repeated iterations
-    // (10 trials each) set the backward launch's tail.
+    // ~1 QP in 3700 stalls this way (numpy oracle, tests/golden/
+    // make_boxqp_stagnation.py), and its ~90 repeated iterations (10 trials
+    // each) set the backward launch's tail.
     if (!moved) break;
   }
   return true;
