@@ -724,6 +724,12 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
     // make_boxqp_stagnation.py), and its ~90 repeated iterations (10 trials
     // each) set the backward launch's tail.
     if (!moved) break;
+    // The next iteration's convergence test without its mat-vec: with no
+    // control clamped now and none at a bound after the step, that
+    // iteration's clamped set is empty again (no refactor, same xsf) and its
+    // step is dx = xsf - x, so when that is below th_grad it stops right
+    // there with this x.  (Otherwise it runs as usual.)
+    if (!(__ballot(cl || x == lb || x == ub) & 0x7Full) && lane0(max8(fabs(xsf - x)) < C.qp_th_grad)) break;
   }
   return true;
 }
