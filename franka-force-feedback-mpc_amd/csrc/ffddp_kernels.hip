@@ -66,6 +66,7 @@ struct InstState {
   int is_feasible, was_feasible, done, ok, iter, recalc, accepted, bw_ok;
   int n_iters, n_trials, n_retries, n_backward, n_calc, n_forward;
   int n_eval1, n_eval2;  // line-search trials evaluated by the first / second pass
+  int n_neg, n_neg_acc;  // trials judged / accepted by the ascent-direction branch (dVexp < 0)
 };
 
 struct Dev {
@@ -162,6 +163,7 @@ __global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __
       s.bw_ok = 0;
       s.n_iters = s.n_trials = s.n_retries = s.n_backward = s.n_calc = s.n_forward = 0;
       s.n_eval1 = s.n_eval2 = 0;
+      s.n_neg = s.n_neg_acc = 0;
       s.ffeas = 0.0;
       d.st[i] = s;
     }
@@ -1859,6 +1861,10 @@ __device__ int accept_instance(const DevConsts& C, Dev& d, int b, int iter, int 
     tdV = e0;
     tdVexp = e1;
     td1 = e2;
+    if (!T.fail[tr] && e1 < 0) {
+      s.n_neg += 1;
+      s.n_neg_acc += okt ? 1 : 0;
+    }
     if (okt) {
       acc = tr;
       steplength = a;
@@ -2003,6 +2009,8 @@ __global__ __launch_bounds__(64) void k_finalize(const DevConsts* __restrict__ C
       stats[(long)b * FFDDP_NSTATS + 5] = s.n_forward;
       stats[(long)b * FFDDP_NSTATS + 6] = s.n_eval1;
       stats[(long)b * FFDDP_NSTATS + 7] = s.n_eval2;
+      stats[(long)b * FFDDP_NSTATS + 8] = s.n_neg;
+      stats[(long)b * FFDDP_NSTATS + 9] = s.n_neg_acc;
     }
   }
   if (fn_pred == nullptr) return;

@@ -44,7 +44,7 @@ SYMBOLS = (
     "ffddp_host_free",
 )
 PLANT_OBS = 69
-NSTATS = 8
+NSTATS = 10
 TRACE_W = 10
 TRACE_FIELDS = ("iter", "cost", "stop", "grad", "preg", "dreg", "step", "ffeas", "dV", "dV_exp")
 NEGSTEP_CROCODDYL = 0

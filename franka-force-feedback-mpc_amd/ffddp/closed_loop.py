@@ -54,8 +54,11 @@ def scenario_settings(name: str) -> dict:
 def run_single(scenario: str = "flat", total_time: float = 20.0, variant: str = "classical",
                results_dir: Path | str = "results/classical_eval", contact_model: str = "normal_1d",
                mpc_iters: Optional[int] = None, circle_radius: float = 0.10, circle_omega: float = 1.5,
-               horizon: Optional[int] = None, device: int = 0, verbose: bool = True, log: bool = True) -> dict:
-    """One closed-loop run; returns the summary dict (and writes the run log)."""
+               horizon: Optional[int] = None, device: int = 0, verbose: bool = True, log: bool = True,
+               neg_step_rule: int = 0) -> dict:
+    """One closed-loop run; returns the summary dict (and writes the run log).
+    neg_step_rule: the solver's ascent-direction comparator (include/ffddp.h
+    FFDDP_NEGSTEP_*; 0 = Crocoddyl's, the reference's behaviour)."""
     settings = scenario_settings(scenario)
     plant = PandaTablePlant(n_substeps=5, timestep=0.001, device=device)
     obs = plant.reset("neutral")
@@ -79,10 +82,12 @@ def run_single(scenario: str = "flat", total_time: float = 20.0, variant: str = 
     max_iters = int(mpc_iters) if mpc_iters is not None else 10
     if variant == "ff":
         cfg = CT.ff_benchmark_config(plant.dt, z_contact, max_iters=max_iters, contact_model=contact_model,
+                                     neg_step_rule=neg_step_rule,
                                      **({"horizon": horizon} if horizon else {}))
         mpc = CT.ForceFeedbackCrocoddylMPC(sim=plant, traj_fn=traj, config=cfg, device=device)
     else:
         cfg = CT.classical_benchmark_config(plant.dt, z_contact, max_iters=max_iters, contact_model=contact_model,
+                                            neg_step_rule=neg_step_rule,
                                             **({"horizon": horizon} if horizon else {}))
         mpc = CT.ClassicalCrocoddylMPC(sim=plant, traj_fn=traj, config=cfg, device=device)
     if abs(settings["tilt_deg"]) > 1e-12:
@@ -98,7 +103,8 @@ def run_single(scenario: str = "flat", total_time: float = 20.0, variant: str = 
                        notes={"scenario": scenario, "scene": "panda_table_scene (ffddp plant stand-in)"}) if log \
         else None
     steps = int(total_time / plant.dt)
-    series = {k: [] for k in ("t", "err_tan", "err_3d", "fn_meas", "fn_pred", "contact")}
+    series = {k: [] for k in ("t", "err_tan", "err_3d", "fn_meas", "fn_pred", "contact", "unstable", "neg_acc",
+                                "not_ok")}
     t = 0.0
     wall0 = time.perf_counter()
     solve_s = 0.0
@@ -118,7 +124,10 @@ def run_single(scenario: str = "flat", total_time: float = 20.0, variant: str = 
         fn_pred = float(info.get("fn_pred", np.nan))
         in_contact = fn_meas > 0.5
         for key, val in (("t", t), ("err_tan", err_tan), ("err_3d", err_3d), ("fn_meas", fn_meas),
-                         ("fn_pred", fn_pred), ("contact", 1.0 if in_contact else 0.0)):
+                         ("fn_pred", fn_pred), ("contact", 1.0 if in_contact else 0.0),
+                         ("unstable", float(bool(info.get("unstable", False)))),
+                         ("neg_acc", float(info.get("neg_accepted", 0))),
+                         ("not_ok", float(bool(info.get("solved_now", False)) and not bool(info.get("ok", False))))):
             series[key].append(val)
         if logger is not None:
             logger.log(
@@ -143,6 +152,13 @@ def run_single(scenario: str = "flat", total_time: float = 20.0, variant: str = 
     wall = time.perf_counter() - wall0
     summ = summary_metrics(series["t"], series["err_tan"], series["err_3d"], series["fn_meas"], series["contact"],
                            float(cfg.fn_des), t_contact_phase)
+    # solver health over the run: ticks whose command fell back to the
+    # instability guard (crocoddyl_classical.py:392-404, logged as
+    # solver_unstable at run_classical.py:480) and solves that accepted a step
+    # through the ascent-direction branch (include/ffddp.h neg_step_rule)
+    neg = np.asarray(series["neg_acc"])
+    summ.update(unstable_ticks=int(np.sum(series["unstable"])), neg_accepted_ticks=int(np.sum(neg > 0)),
+                neg_accepted_total=int(np.sum(neg)), solve_not_ok_ticks=int(np.sum(series["not_ok"])))
     summ.update(total_time=float(total_time), dt=float(plant.dt), scenario_label=settings["label"],
                 scenario_tilt_deg=float(settings["tilt_deg"]), uncertainty_profile=unc_meta,
                 torque_scale=settings["torque_scale"].tolist(), fn_des=float(cfg.fn_des),
@@ -177,12 +193,15 @@ def main(argv=None):
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--circle-radius", type=float, default=0.10)
     ap.add_argument("--circle-omega", type=float, default=1.5)
+    ap.add_argument("--neg-step-rule", type=int, choices=(0, 1), default=0,
+                    help="ascent-direction comparator: 0 Crocoddyl's (default), 1 bounded rise")
     args = ap.parse_args(argv)
     names = SCENARIOS if args.scenario == "all" else (args.scenario,)
     out = {}
     for name in names:
         out[name] = run_single(name, args.time, args.variant, args.results_dir, args.contact_model, args.mpc_iters,
-                               args.circle_radius, args.circle_omega, args.horizon)
+                               args.circle_radius, args.circle_omega, args.horizon,
+                               neg_step_rule=args.neg_step_rule)
     return out
 
 

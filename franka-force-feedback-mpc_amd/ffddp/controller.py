@@ -95,6 +95,11 @@ class ClassicalMPCConfig:
     max_tau_raw_inf: float = 3.0e2
     fallback_dq_damping: float = 5.0
     contact_release_steps: int = 25
+    # Not a field of the reference's config: the comparator of the solver's
+    # ascent-direction acceptance (include/ffddp.h FFDDP_NEGSTEP_*), which the
+    # reference leaves at Crocoddyl's own (0).  1 = bounded rise; its effect on
+    # the closed loop is in DESIGN.md §3.
+    neg_step_rule: int = 0
 
 
 @dataclass
@@ -128,7 +133,8 @@ class ForceFeedbackMPCConfig(ClassicalMPCConfig):
 
 
 def classical_benchmark_config(dt: float, z_contact: float, max_iters: int = 10, horizon: int = 36,
-                               contact_model: str = "normal_1d", phase_source: str = "trajectory"):
+                               contact_model: str = "normal_1d", phase_source: str = "trajectory",
+                               neg_step_rule: int = 0):
     """Benchmark-mode ClassicalMPCConfig of src/run/run_classical.py:269-315."""
     return ClassicalMPCConfig(
         horizon=horizon, dt=dt, dt_ocp=0.01, z_contact=z_contact, z_press=0.0065, w_ee_pos=1.2e3,
@@ -140,13 +146,13 @@ def classical_benchmark_config(dt: float, z_contact: float, max_iters: int = 10,
         w_wdamp_weights=np.array([1.8, 1.8, 0.3]), fn_contact_on=1.0, fn_contact_off=0.1, z_contact_band=0.012,
         max_iters=max_iters, mpc_update_steps=1, use_feedback_policy=True, feedback_gain_scale=0.55,
         max_solver_cost=1.0e8, max_tau_raw_inf=3.0e2, contact_release_steps=60, contact_model=contact_model,
-        phase_source=phase_source, apply_command_filter=False, debug_every=100,
+        phase_source=phase_source, apply_command_filter=False, debug_every=100, neg_step_rule=neg_step_rule,
     )
 
 
 def ff_benchmark_config(dt: float, z_contact: float, max_iters: int = 10, horizon: int = 40,
                         contact_model: str = "normal_1d", phase_source: str = "trajectory",
-                        ff_tau_state_source: str = "tau_meas_act_filt"):
+                        ff_tau_state_source: str = "tau_meas_act_filt", neg_step_rule: int = 0):
     """Benchmark-mode ForceFeedbackMPCConfig of src/run/run_force_feedback.py:272-330."""
     return ForceFeedbackMPCConfig(
         horizon=horizon, dt=dt, dt_ocp=0.01, z_contact=z_contact, z_press=0.0065, w_ee_pos=1.2e3,
@@ -162,7 +168,7 @@ def ff_benchmark_config(dt: float, z_contact: float, max_iters: int = 10, horizo
         use_feedback_policy=True, feedback_gain_scale=0.55, max_solver_cost=1.0e8, max_tau_raw_inf=3.0e2,
         contact_release_steps=80, contact_model=contact_model, phase_source=phase_source,
         apply_command_filter=False, ff_tau_state_source=ff_tau_state_source, ff_cutoff_hz=25.0,
-        ff_inverse_actuation_model=True, ff_tau_feedback_gain=1.0, debug_every=500,
+        ff_inverse_actuation_model=True, ff_tau_feedback_gain=1.0, debug_every=500, neg_step_rule=neg_step_rule,
     )
 
 
@@ -216,6 +222,7 @@ class _MPCBase:
         self._last_solve_ok = False
         self._last_solve_cost = np.nan
         self._last_solve_iters = -1
+        self._last_neg = (0, 0)
         self._surface_latched = False
         self._contact_loss_count = 0
         self._prev_surface_mode: Optional[bool] = None
@@ -223,6 +230,7 @@ class _MPCBase:
                           "surface_mode": False, "unstable": False, "fn_pred": np.nan}
         self.ocp = self._ocp_config()
         self._solver = BatchedBoxFDDP(self.ocp, max_batch=1, device=device)
+        self._solver.neg_step_rule = int(getattr(self.cfg, "neg_step_rule", 0))
         if self.cfg.verbose:  # crocoddyl_classical.py:352-353, 360-361
             self._solver.setCallbacks([CallbackVerbose()], max_iters=max(int(self.cfg.max_iters), 1))
 
@@ -365,6 +373,9 @@ class _MPCBase:
         ok = bool(s.solve(prob, maxiter=int(self.cfg.max_iters), is_feasible=False,
                           xs_init=np.asarray(xs_init)[None], us_init=np.asarray(us_init)[None])[0])
         cost, iters = float(s.cost[0]), int(s.iter[0])
+        st = getattr(s, "stats", None)
+        # ascent-direction branch (dVexp < 0): trials judged / accepted in this solve
+        self._last_neg = (int(st[0, 8]), int(st[0, 9])) if st is not None and st.shape[1] > 9 else (0, 0)
         self._last_solve_step = self._k
         self._last_solve_ok, self._last_solve_cost, self._last_solve_iters = ok, cost, iters
         if N > 0 and np.all(np.isfinite(s.us[0, 0])):
@@ -452,6 +463,7 @@ class ClassicalCrocoddylMPC(_MPCBase):
             "tau_cmd_inf": float(np.max(np.abs(tau_cmd))), "surface_mode": bool(surface_now),
             "unstable": bool(unstable), "fn_pred": float(fn_pred) if np.isfinite(fn_pred) else np.nan,
             "solved_now": bool(solved_now), "policy_idx": int(policy_idx),
+            "neg_branch": self._last_neg[0] if solved_now else 0, "neg_accepted": self._last_neg[1] if solved_now else 0,
         }
         if (self._k % self.cfg.debug_every) == 0:  # crocoddyl_classical.py:420-428
             fn = float(getattr(obs, "f_contact_normal", 0.0))
@@ -682,6 +694,7 @@ class ForceFeedbackCrocoddylMPC(_MPCBase):
             "tau_cmd_inf": float(np.max(np.abs(tau_cmd))), "surface_mode": bool(surface_now),
             "unstable": bool(unstable), "fn_pred": fin(fn_pred), "fn_pred_raw": fin(fn_pred_raw),
             "fn_pred_corr": fin(self._fn_pred_corr), "solved_now": bool(solved_now), "policy_idx": int(policy_idx),
+            "neg_branch": self._last_neg[0] if solved_now else 0, "neg_accepted": self._last_neg[1] if solved_now else 0,
         }
         if (self._k % self.cfg.debug_every) == 0:  # crocoddyl_force_feedback.py:673-683
             fn = float(getattr(obs, "f_contact_normal", 0.0))

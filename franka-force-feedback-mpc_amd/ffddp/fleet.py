@@ -72,6 +72,7 @@ class FleetClassicalMPC:
             setattr(ocp, f, getattr(cfg, f))
         ocp.tau_limits = np.asarray(cfg.tau_limits, float).copy()
         self.solver = BatchedBoxFDDP(ocp, max_batch=self.B, device=device)
+        self.solver.neg_step_rule = int(getattr(cfg, "neg_step_rule", 0))
         f64 = dict(dtype=torch.float64, device=self.dev)
         B, N = self.B, self.N
         self.T = dict(
@@ -169,6 +170,7 @@ class FleetClassicalMPC:
         cost = T["cost"].cpu().numpy()
         iters = T["iters"].cpu().numpy()
         ok = T["ok"].cpu().numpy().astype(bool)
+        neg_acc = T["stats"][:, 9].cpu().numpy()  # ascent-direction acceptances of this solve
         fn_pred = np.where(surface_now, T["fn_pred"][:, 0].cpu().numpy(), np.nan)
         # _policy_control (:759-779): u = us[0] + s K[0] (x - xs[0])
         tau_raw = np.where(self.valid[:, None], us0, self.tau_prev)
@@ -188,7 +190,8 @@ class FleetClassicalMPC:
         self.tau_prev = tau_cmd.copy()
         self.last_info = dict(ok=ok, cost=cost, iters=iters, tau_raw_inf=tau_raw_inf,
                               tau_cmd_inf=np.max(np.abs(tau_cmd), 1), surface_mode=surface_now, unstable=unstable,
-                              fn_pred=fn_pred, solved_now=np.ones(B, bool), policy_idx=policy_idx)
+                              fn_pred=fn_pred, solved_now=np.ones(B, bool), policy_idx=policy_idx,
+                              neg_accepted=neg_acc)
         return tau_cmd
 
 
@@ -217,13 +220,16 @@ def _sweep_instances(scenarios: Sequence[str], seeds: int):
 
 def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilted_15", "actuation_uncertainty"),
               seeds: int = 256, total_time: float = 4.0, rank: int = 0, world: int = 1, device: int = 0,
-              q_sigma: float = 0.02, verbose: bool = True, record: Sequence[int] = ()) -> dict:
+              q_sigma: float = 0.02, verbose: bool = True, record: Sequence[int] = (),
+              neg_step_rule: int = 0) -> dict:
     """Closed-loop sweep of len(scenarios) * seeds instances; this rank runs
     its contiguous shard.  Returns per-instance summary arrays (this shard).
     record: shard-local instance indices whose controller inputs (the plant
     record as the controller sees it, after any measurement noise) and
     commanded torques are kept per tick, with what a scalar controller needs
-    to replay them (the task, the config, the start states)."""
+    to replay them (the task, the config, the start states).
+    neg_step_rule: the solver's ascent-direction comparator (include/ffddp.h
+    FFDDP_NEGSTEP_*; 0 = Crocoddyl's, the reference's behaviour)."""
     names, tilt, scale, seed = _sweep_instances(scenarios, seeds)
     n_all = len(names)
     per = (n_all + world - 1) // world
@@ -255,7 +261,7 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
     plant.set_tilt(0.0)
     plant.step(np.zeros((B, 7)), integrate=False)  # mj_forward at the start state
     tau0 = plant.obs[:, 14:21].copy()
-    cfg = classical_benchmark_config(plant.dt, z_contact)
+    cfg = classical_benchmark_config(plant.dt, z_contact, neg_step_rule=neg_step_rule)
     mpc = FleetClassicalMPC(B, traj, cfg, q_nom=q0, tau0=tau0, R_site_from_pin_ee=R_site_from_pin_ee,
                             p_site_minus_frame_pin=p_off, device=device)
     plant.set_tilt(tilt)  # hidden from the controllers
@@ -267,6 +273,13 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
             inj[b] = ScenarioUncertaintyInjector(dt=plant.dt, nu=7, config=uc)
     steps = int(total_time / plant.dt)
     series = {k: np.zeros((steps, B)) for k in ("t", "err_tan", "err_3d", "fn_meas", "contact")}
+    # solver health per instance: ticks on the instability fallback
+    # (crocoddyl_classical.py:392-404; solver_unstable, run_classical.py:480)
+    # ticks whose solve accepted an ascent-direction step and ticks whose
+    # solve returned ok = False
+    unstable_ticks = np.zeros(B)
+    neg_ticks = np.zeros(B)
+    not_ok_ticks = np.zeros(B)
     rec_idx = [int(i) for i in record]
     rec_obs = np.zeros((steps, len(rec_idx), plant.obs.shape[1]))
     rec_tau = np.zeros((steps, len(rec_idx), 7))
@@ -286,6 +299,9 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
         tc = time.perf_counter()
         tau = mpc.compute_control(q, v, bias, fn, ee[:, 2], t)
         ctrl_s += time.perf_counter() - tc
+        unstable_ticks += mpc.last_info["unstable"]
+        neg_ticks += mpc.last_info["neg_accepted"] > 0
+        not_ok_ticks += ~mpc.last_info["ok"]
         if rec_idx:
             rec_t[k] = t
             rec_obs[k] = obs[rec_idx]
@@ -310,14 +326,16 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
     wall = time.perf_counter() - wall0
     mpc.close()
     plant.close()
-    keys = ("rms_tangential_error", "rms_tangential_error_contact_phase", "rms_3d_error", "avg_abs_force_err",
-            "max_fn", "contact_loss_contact_phase_pct", "fn_mean_contact_phase")
-    per_inst = {k: np.zeros(B) for k in keys}
+    keys = SUMMARY_KEYS[:-3]
+    per_inst = {k: np.zeros(B) for k in SUMMARY_KEYS}
     for b in range(B):
         s = summary_metrics(series["t"][:, b], series["err_tan"][:, b], series["err_3d"][:, b],
                             series["fn_meas"][:, b], series["contact"][:, b], float(cfg.fn_des), t_cp)
         for k_ in keys:
             per_inst[k_][b] = s[k_]
+    per_inst["unstable_ticks"] = unstable_ticks
+    per_inst["neg_accepted_ticks"] = neg_ticks
+    per_inst["solve_not_ok_ticks"] = not_ok_ticks
     out = dict(names=names, seed=seed, per_instance=per_inst, ticks=steps, wall_s=wall, controller_s=ctrl_s,
                instances=B, shard=(lo, hi), n_all=n_all)
     if rec_idx:
@@ -327,7 +345,8 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
 
 
 SUMMARY_KEYS = ("rms_tangential_error", "rms_tangential_error_contact_phase", "rms_3d_error", "avg_abs_force_err",
-                "max_fn", "contact_loss_contact_phase_pct", "fn_mean_contact_phase")
+                "max_fn", "contact_loss_contact_phase_pct", "fn_mean_contact_phase", "unstable_ticks",
+                "neg_accepted_ticks", "solve_not_ok_ticks")
 
 
 def gather_summaries(res: dict, n_all: int, device=None):

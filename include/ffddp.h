@@ -32,7 +32,7 @@ extern "C" {
 #define FFDDP_NQ 7      /* Panda arm joints (fingers locked, crocoddyl_classical.py:189-197) */
 #define FFDDP_NU 7      /* ActuationModelFull: nu = nv (:147) */
 #define FFDDP_MAX_NC 3  /* ContactModel1D (nc=1) or ContactModel3D (nc=3) */
-#define FFDDP_NSTATS 8  /* per-instance counters returned by the solve */
+#define FFDDP_NSTATS 10 /* per-instance counters returned by the solve */
 #define FFDDP_NKERNELS 9 /* kernel classes reported by ffddp_profile_read */
 
 enum {
@@ -145,7 +145,10 @@ const char* ffddp_last_error(const ffddp_handle* h);
  *                    instance (first pass + second pass when it ran),
  *                    [6] / [7] step lengths evaluated by the first / second
  *                    line-search pass — for the roofline byte count
- *                    (SURVEY.md §8(d)). */
+ *                    (SURVEY.md §8(d)),
+ *                    [8] / [9] line-search trials judged / accepted by the
+ *                    ascent-direction branch (dVexp < 0, see
+ *                    ffddp_solver_params.neg_step_rule). */
 int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* node_ref,
                       const double* inst_ref, const uint8_t* surface, const double* xs_init,
                       const double* us_init, int maxiter, int is_feasible, double* xs, double* us,

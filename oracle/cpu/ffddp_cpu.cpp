@@ -119,6 +119,7 @@ struct Inst {
   double cost = 0.0, preg = 0.0, dg = 0.0, dq = 0.0, stop = 0.0;
   bool feas = false;
   int n_iters = 0, n_trials = 0, n_retries = 0, n_backward = 0, n_calc = 0, n_forward = 0;
+  int n_neg = 0, n_neg_acc = 0;  // trials judged / accepted by the ascent-direction branch (dVexp < 0)
 
   void init(const DevConsts& c) {
     C = &c;
@@ -549,6 +550,10 @@ bool solve_one(const DevConsts& C, Inst& I, int maxiter, int& iter_out) {
       const bool ok = dVexp >= 0 ? (std::fabs(d0) < C.th_grad || dV > C.th_acceptstep * dVexp)
                                  : (!I.feas && (C.neg_rule == FFDDP_NEGSTEP_CROCODDYL ? dV < C.th_acceptnegstep * dVexp
                                                                                        : dV > C.th_acceptnegstep * dVexp));
+      if (dVexp < 0) {
+        I.n_neg += 1;
+        I.n_neg_acc += ok ? 1 : 0;
+      }
       if (ok) {
         was_feasible = I.feas;
         I.xs.swap(I.xs_try);
@@ -591,6 +596,7 @@ int solve_batch_t(const DevConsts& C, int B, const double* x0, const double* nre
       std::copy(xs_init + (size_t)b * (N + 1) * nx, xs_init + (size_t)(b + 1) * (N + 1) * nx, I.xs.begin());
       std::copy(us_init + (size_t)b * N * NU, us_init + (size_t)(b + 1) * N * NU, I.us.begin());
       I.n_iters = I.n_trials = I.n_retries = I.n_backward = I.n_calc = I.n_forward = 0;
+      I.n_neg = I.n_neg_acc = 0;
       I.cost = 0.0;
       int it = 0;
       const bool res = solve_one<NC, FF>(C, I, maxiter, it);
@@ -610,6 +616,8 @@ int solve_batch_t(const DevConsts& C, int B, const double* x0, const double* nre
         s[5] = I.n_forward;
         s[6] = I.n_trials;
         s[7] = 0;
+        s[8] = I.n_neg;
+        s[9] = I.n_neg_acc;
       }
     }
   }

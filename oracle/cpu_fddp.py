@@ -16,7 +16,7 @@ from pathlib import Path
 import numpy as np
 
 LIB = Path(__file__).resolve().parent / "cpu" / "libffddp_cpu.so"
-NSTATS = 8
+NSTATS = 10
 _lib = None
 
 

@@ -55,6 +55,13 @@ def rel_err(a, b):
     return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
 
 
+def elem_err(a, b):
+    """Largest element-wise error |a - b| / (1 + |b|): unlike rel_err, small
+    entries of a block with large ones (K: 1e-3 .. 1e3) keep their own scale."""
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.max(np.abs(a - b) / (1.0 + np.abs(b)))) if a.size else 0.0
+
+
 def log_parity(case: str, **fields):
     """Append one JSON line with the observed errors of a parity case to
     $FFDDP_PARITY_LOG (when set), so the tolerances can be set from data."""
@@ -69,3 +76,34 @@ def log_parity(case: str, **fields):
         rec[k] = v.item() if hasattr(v, "item") else v
     with open(path, "a") as f:
         f.write(json.dumps(rec) + "\n")
+
+
+# closed-loop outcome pins (tests/golden/closed_loop_outcome.json): error and
+# count metrics within a factor OUTCOME_BAND of the committed value (both
+# ways: a change of the closed loop's behaviour is news either way), contact
+# loss within OUTCOME_LOSS_PP percentage points, instability fallbacks exact
+OUTCOME_BAND = 1.25
+OUTCOME_LOSS_PP = 1.0
+
+
+def closed_loop_pins():
+    import json
+    from pathlib import Path
+
+    return json.loads((Path(__file__).resolve().parent / "golden" / "closed_loop_outcome.json").read_text())
+
+
+def check_outcome(got: dict, pin: dict, tag: str):
+    for k, ref in pin.items():
+        v = float(got[k])
+        if k.startswith("contact_loss"):
+            assert abs(v - ref) <= OUTCOME_LOSS_PP, (tag, k, v, ref)
+        elif k.startswith("unstable"):
+            assert v == ref, (tag, k, v, ref)
+        elif ref == 0:
+            assert v <= 3, (tag, k, v, ref)
+        else:
+            lo, hi = ref / OUTCOME_BAND, ref * OUTCOME_BAND
+            if k.endswith("_ticks") or k.endswith("_ticks_mean"):  # counts: +-3 ticks of slack besides the band
+                lo, hi = lo - 3, hi + 3
+            assert lo <= v <= hi, (tag, k, v, ref)

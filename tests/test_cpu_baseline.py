@@ -32,6 +32,7 @@ def test_cpu_baseline_matches_oracle(variant, contact, surf, regime, tol):
     for i, r in enumerate(ref):
         assert bool(out["ok"][i]) == r["ok"] and int(out["iter"][i]) == r["iter"]
         assert int(out["stats"][i, 1]) == r["trials"] and int(out["stats"][i, 2]) == r["reg_retries"]
+        assert int(out["stats"][i, 8]) == r["neg_branch"] and int(out["stats"][i, 9]) == r["neg_accepted"]
         for k in ("xs", "us", "K"):
             assert rel_err(out[k][i], r[k]) < tol, (k, i, rel_err(out[k][i], r[k]))
         assert rel_err(out["cost"][i], r["cost"]) < tol

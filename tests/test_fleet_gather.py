@@ -61,9 +61,12 @@ def test_gather_summaries_two_ranks():
         p.join(60)
         assert p.exitcode == 0
     n = len(names)
-    assert m.shape == (n, 7)
+    from ffddp import fleet
+
+    nk = len(fleet.SUMMARY_KEYS)
+    assert m.shape == (n, nk)
     ids = np.arange(n, dtype=float)
-    for j in range(7):
+    for j in range(nk):
         np.testing.assert_array_equal(m[:, j], ids * 10 + j)
     assert list(table) == list(SCEN)
     assert table["flat"]["instances"] == seeds

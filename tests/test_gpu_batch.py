@@ -18,7 +18,7 @@ import pytest
 
 from ffddp import BatchedBoxFDDP, FfddpError
 
-from helpers import log_parity, make_batch, oracle_cfg, oracle_problem, oracle_solve, product_cfg, rel_err
+from helpers import elem_err, log_parity, make_batch, oracle_cfg, oracle_problem, oracle_solve, product_cfg, rel_err
 from oracle_pool import solve_many
 
 pytestmark = pytest.mark.gpu
@@ -33,12 +33,27 @@ def _sub(batch, idx):
     return b
 
 
-@pytest.mark.parametrize("variant,B", [("classical", 4096), ("classical", 517), ("ff", 1024)])
-def test_full_batch_equals_small_batches(variant, B, monkeypatch):
-    """classical B = 4096: the metric's batch; FF B = 1024: BASELINE configs[2]."""
+# regime -> (xs/us/cost, K, K element-wise) tolerance of the oracle spread:
+# tracking as the parity cases (observed <= 1.3e-11,
+# profiles/r02_parity_errors.jsonl); random x0 (unconverged 10-iteration
+# solves from far-off starts) at its error budget: against an x87
+# extended-precision solve of the same 8 instances the numpy oracle itself
+# is 1.7e-7 off in us, 1.4e-8 in K (9.9e-7 element-wise), the C++ baseline
+# 2.2e-7 / 3.7e-8 / 3.1e-6 (tools/ext_budget.py, profiles/r04_ext_budget.jsonl)
+SPREAD_TOL = {"tracking": (1e-10, 3e-10, 1e-5), "random": (2e-7, 2e-7, 1e-5)}
+
+
+@pytest.mark.parametrize("variant,B,regime", [("classical", 4096, "tracking"), ("classical", 517, "tracking"),
+                                              ("classical", 1024, "random"), ("ff", 1024, "tracking")])
+def test_full_batch_equals_small_batches(variant, B, regime, monkeypatch):
+    """classical B = 4096: the metric's batch; classical B = 1024 random x0:
+    BASELINE configs[1] (crocoddyl_classical.py:367 solve semantics; the
+    SURVEY-literal draw around the neutral keyframe, panda_robot.xml:233),
+    where the device-side line-search widening, the BoxQP stall exit and the
+    four-slice schedule all switch on; FF B = 1024: BASELINE configs[2]."""
     N = 30
     cfg = product_cfg(variant, N)
-    batch = make_batch(variant, B, N, seed=77)
+    batch = make_batch(variant, B, N, seed=77, regime=regime)
     big = BatchedBoxFDDP(cfg, max_batch=B)
     big.solve(batch, maxiter=10)
     # one-stream reference solver for small batches
@@ -53,19 +68,28 @@ def test_full_batch_equals_small_batches(variant, B, monkeypatch):
             for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred"):
                 a, b = getattr(big, name)[i], getattr(small, name)[j]
                 assert np.array_equal(a, b, equal_nan=True), (name, int(i))
+            # the counters, except [5..7] (which line-search pass evaluated a
+            # trial depends on the slice's active count, not on the instance)
+            sa, sb = big.stats[i], small.stats[j]
+            assert np.array_equal(sa[[0, 1, 2, 3, 4, 8, 9]], sb[[0, 1, 2, 3, 4, 8, 9]]), int(i)
     # a spread of them against the oracle
     sel = picks[::2]
     ref = solve_many(cfg, batch, sel)
-    e = dict(xs=0.0, us=0.0, cost=0.0)
+    e = dict(xs=0.0, us=0.0, cost=0.0, K=0.0, K_elem=0.0)
     for i, r in zip(sel, ref):
         assert bool(big.ok[i]) == r["ok"] and int(big.iter[i]) == r["iter"]
+        assert int(big.stats[i, 1]) == r["trials"] and int(big.stats[i, 2]) == r["reg_retries"]
+        assert int(big.stats[i, 8]) == r["neg_branch"] and int(big.stats[i, 9]) == r["neg_accepted"]
         e["xs"] = max(e["xs"], rel_err(big.xs[i], r["xs"]))
         e["us"] = max(e["us"], rel_err(big.us[i], r["us"]))
         e["cost"] = max(e["cost"], rel_err(big.cost[i], r["cost"]))
-    log_parity(f"batch/{variant}/B{B}", n=len(sel), **e)
-    assert max(e.values()) < 1e-10, e  # observed <= 1.3e-11 (profiles/r02_parity_errors.jsonl)
+        e["K"] = max(e["K"], rel_err(big.K[i], r["K"]))
+        e["K_elem"] = max(e["K_elem"], elem_err(big.K[i], r["K"]))
+    log_parity(f"batch/{variant}/{regime}/B{B}", n=len(sel), **e)
+    tol, tol_k, tol_ke = SPREAD_TOL[regime]
+    assert max(e["xs"], e["us"], e["cost"]) < tol and e["K"] < tol_k and e["K_elem"] < tol_ke, e
     assert np.all(np.isfinite(big.cost))
-    if variant == "classical":
+    if variant == "classical" and regime == "tracking":
         assert np.mean(big.ok) > 0.9
     big.close()
     small.close()

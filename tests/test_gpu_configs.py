@@ -7,6 +7,9 @@
   bounds in every scenario) and three instances from different scenarios
   replayed tick for tick through the scalar ClassicalCrocoddylMPC (B = 1
   solves, ffddp.controller) at 1e-7.
+* configs[3] / configs[0] closed-loop outcome (task metrics, instability
+  fallbacks, not-ok solves) under both ascent-direction comparators, pinned
+  against the committed runs (test_c4_outcome, test_c1_flat_outcome).
 * configs[4] per-GPU shape — horizon 100, point3d, B = 1024 (the 8192-instance
   batch over 8 GPUs): every checked instance equals, bit for bit, the same
   instance solved in a batch of 8 on one stream, and a spread of them
@@ -24,7 +27,7 @@ from ffddp import controller as CT  # noqa: E402
 from ffddp import fleet as FL  # noqa: E402
 from ffddp import plant as PL  # noqa: E402
 
-from helpers import log_parity, make_batch, product_cfg, rel_err  # noqa: E402
+from helpers import check_outcome, closed_loop_pins, log_parity, make_batch, product_cfg, rel_err  # noqa: E402
 from oracle_pool import solve_many  # noqa: E402
 
 
@@ -60,6 +63,40 @@ def test_c4_full_sweep_1280_instances():
         ctrl.close()
         sim.close()
     log_parity("c4_sweep/1280/replay3", worst_tau=worst, ticks=out["ticks"], wall_s=out["wall_s"])
+
+
+@pytest.mark.parametrize("rule", [0, 1])
+def test_c4_outcome(rule):
+    """configs[3] at its length (5 x 256 closed loops, 4 s each) under each
+    ascent-direction comparator: per scenario, the median RMS tangential
+    error (whole run and contact phase), the median force error, the mean
+    contact loss, the instability fallbacks and the not-ok solves against
+    the committed run (tests/golden/closed_loop_outcome.json, helpers.
+    check_outcome).  Round 3's unnoticed regression (flat contact-phase
+    median 7.3 -> 19.8 mm when the default comparator changed) fails this."""
+    out = FL.run_sweep(seeds=256, total_time=4.0, verbose=False, neg_step_rule=rule)
+    pins = closed_loop_pins()[f"gpu_c4_4s_rule{rule}"]
+    pi, names = out["per_instance"], out["names"]
+    for s, pin in pins.items():
+        sel = names == s
+        got = {}
+        for key in pin:
+            metric, stat = key.rsplit("_", 1)
+            got[key] = np.median(pi[metric][sel]) if stat == "median" else np.mean(pi[metric][sel])
+        log_parity(f"c4_outcome/rule{rule}/{s}", **got)
+        check_outcome(got, pin, f"c4/rule{rule}/{s}")
+
+
+@pytest.mark.parametrize("rule", [0, 1])
+def test_c1_flat_outcome(rule):
+    """configs[0] (flat, 20 s, one robot: HIP solver + HIP plant) under each
+    comparator against the committed run."""
+    from ffddp.closed_loop import run_single
+
+    s = run_single("flat", 20.0, verbose=False, log=False, neg_step_rule=rule)
+    pin = closed_loop_pins()[f"gpu_c1_flat_20s_rule{rule}"]
+    log_parity(f"c1_outcome/rule{rule}", **{k: s[k] for k in pin})
+    check_outcome(s, pin, f"c1/rule{rule}")
 
 
 def _sub(batch, idx):

@@ -16,7 +16,7 @@ significands the two forms agree to ~1e-15).
 max |impl - ext| / max(1, max |ext|) over xs, us, K, cost; one JSON line per
 case.  Oracle / test infrastructure only.
 
-usage: python tools/ext_budget.py OUT.jsonl [GPU.npz]
+usage: python tools/ext_budget.py OUT.jsonl [GPU.npz] [CASE-NAME-PREFIX]
 """
 from __future__ import annotations
 
@@ -38,7 +38,16 @@ CASES = [
     ("solve/ff/point3d/surf1/cone1", "ff", "point3d", 1, 12, 4, 22, 1, "tracking"),
     ("solve/point3d/N100", "classical", "point3d", 0, 100, 2, 55, 1, "tracking"),
     ("solve/random/N30/B32[:8]", "classical", "normal_1d", 0, 30, 8, 101, None, "random"),
+    # tests/test_gpu_batch.py's oracle spread of configs[1] (B = 1024 random x0, seed 77)
+    ("batch/classical/random/B1024[spread]", "classical", "normal_1d", 0, 30, 8, 77, None, "random"),
 ]
+
+
+def spread_picks(B):
+    """The instances tests/test_gpu_batch.py compares with the oracle."""
+    rng = np.random.default_rng(1)
+    picks = np.unique(np.concatenate([[0, 1, B // 4 - 1, B // 4, B // 2, B - 1], rng.integers(0, B, 10)]))
+    return picks[::2]
 
 
 def case_inputs(case):
@@ -48,7 +57,13 @@ def case_inputs(case):
     cfg = product_cfg(variant, N, contact)
     if cone:
         cfg.w_friction_cone, cfg.mu = 2.0e2, 0.6
-    if name.startswith("solve/random"):
+    if name.startswith("batch/"):
+        full = make_batch(variant, 1024, N, seed=seed, regime=regime)
+        idx = spread_picks(1024)[:B]
+        for f in ("x0", "node_ref", "inst_ref", "surface", "xs_init", "us_init", "t0"):
+            setattr(full, f, np.ascontiguousarray(getattr(full, f)[idx]))
+        b = full
+    elif name.startswith("solve/random"):
         b = make_batch(variant, 32, N, seed=seed, regime=regime).slice(slice(0, B))
     else:
         b = make_batch(variant, B, N, seed=seed, surface=surf, regime=regime)
@@ -73,6 +88,13 @@ def err(a, ref):
     return float(np.max(np.abs(a - ref)) / max(1.0, float(np.max(np.abs(ref)))))
 
 
+def err_elem(a, ref):
+    """element-wise |a - ref| / (1 + |ref|) (tests/helpers.py elem_err)"""
+    a = np.asarray(a, np.longdouble)
+    ref = np.asarray(ref, np.longdouble)
+    return float(np.max(np.abs(a - ref) / (1.0 + np.abs(ref))))
+
+
 def main():
     from concurrent.futures import ProcessPoolExecutor
     from multiprocessing import get_context
@@ -81,10 +103,13 @@ def main():
     from oracle import cpu_fddp
 
     out_path = Path(sys.argv[1])
-    gpu = dict(np.load(sys.argv[2])) if len(sys.argv) > 2 else None
+    gpu = dict(np.load(sys.argv[2])) if len(sys.argv) > 2 and sys.argv[2] else None
     lines = []
     with ProcessPoolExecutor(max_workers=8, mp_context=get_context("spawn")) as ex:
+        only = sys.argv[3] if len(sys.argv) > 3 else ""
         for case in CASES:
+            if not case[0].startswith(only):
+                continue
             t0 = time.time()
             cfg, b = case_inputs(case)
             B = b.B
@@ -112,6 +137,8 @@ def main():
                     e = max(err(im[k][i], ext[i][k]) for i in range(B) if rec["same_path"][i]) \
                         if any(rec["same_path"]) else None
                     rec[name][k] = e
+                rec[name]["K_elem"] = max(err_elem(im["K"][i], ext[i]["K"]) for i in range(B) if rec["same_path"][i]) \
+                    if any(rec["same_path"]) else None
             # oracle vs cpu vs gpu pairwise, for reference
             if "gpu" in impls:
                 for ref in ("oracle", "oracle_solve"):

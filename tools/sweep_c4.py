@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--seeds", type=int, default=256)
     ap.add_argument("--time", type=float, default=4.0)
     ap.add_argument("--out", type=str, default="")
+    ap.add_argument("--neg-step-rule", type=int, choices=(0, 1), default=0,
+                    help="ascent-direction comparator: 0 Crocoddyl's (default), 1 bounded rise")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -35,7 +37,8 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    res = fleet.run_sweep(seeds=a.seeds, total_time=a.time, rank=rank, world=world, device=local, verbose=(rank == 0))
+    res = fleet.run_sweep(seeds=a.seeds, total_time=a.time, rank=rank, world=world, device=local, verbose=(rank == 0),
+                           neg_step_rule=a.neg_step_rule)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -45,6 +48,7 @@ def main():
                                             a.seeds)
     if rank == 0:
         line = {"config": "5 scenarios x %d seeds closed loop, %.1f s each" % (a.seeds, a.time), "ranks": world,
+                "neg_step_rule": a.neg_step_rule,
                 "instances": int(res["n_all"]), "ticks": res["ticks"], "wall_s": wall,
                 "closed_loop_ticks_per_s": res["n_all"] * res["ticks"] / wall,
                 "rank0_controller_s": res["controller_s"], "scenarios": fleet.scenario_table(names, m)}
