@@ -42,44 +42,23 @@ template <int CTRL> __device__ __forceinline__ double dpp64(double v) {
 template <int CTRL> __device__ __forceinline__ int dpp32(int v) {
   return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true);
 }
-#ifndef G8_DPP
-#define G8_DPP 2
-#endif
-// Broadcast of group lane K.  Default (G8_DPP 2): row_newbcast of lane K and
-// of lane 8 + K under bank masks (one v_mov_b64_dpp each: both 8-lane groups
-// of the 16-lane DPP row get their own lane K); faster line search than
-// ds_swizzle BROADCAST(8, K) (G8_DPP 0), which goes through the LDS pipe.
-// G8_DPP 1: quad_perm [k,k,k,k] then row_shr:4 / row_shl:4 under a bank
-// mask (four 32-bit DPP moves; no faster than the swizzle).
+// Broadcast of group lane K: row_newbcast of lane K and of lane 8 + K under
+// bank masks (one v_mov_b64_dpp each: both 8-lane groups of the 16-lane DPP
+// row get their own lane K).  Measured faster in the line search than
+// ds_swizzle BROADCAST(8, K) through the LDS pipe, and than four 32-bit
+// quad_perm / row_shr moves (negative results).
 template <int K> __device__ __forceinline__ double g8_rowb(double v) {
   const long long x = __builtin_bit_cast(long long, v);
   const long long r = __builtin_amdgcn_update_dpp(x, x, 0x150 + K, 0xf, 0xf, true);
   return __builtin_bit_cast(double, r);
 }
 template <int K> __device__ __forceinline__ double g8_bc(double v) {
-#if G8_DPP == 2
-  // both groups of the 16-lane DPP row: row_newbcast of lane 8 + K into
-  // banks 2-3 (lanes 8..15), then of lane K into banks 0-1 (lanes 0..7) of
-  // the same register: two v_mov_b64_dpp, no select
+  // row_newbcast of lane 8 + K into banks 2-3 (lanes 8..15), then of lane K
+  // into banks 0-1 (lanes 0..7) of the same register: two v_mov_b64_dpp, no select
   const long long x = __builtin_bit_cast(long long, v);
   const long long t = __builtin_amdgcn_mov_dpp(x, 0x158 + K, 0xf, 0xC, false);
   const long long r = __builtin_amdgcn_update_dpp(t, x, 0x150 + K, 0xf, 0x3, false);
   return __builtin_bit_cast(double, r);
-#elif G8_DPP
-  constexpr int qp = (K & 3) * 0x55;
-  constexpr int sh = K < 4 ? 0x114 : 0x104;
-  constexpr int bm = K < 4 ? 0xA : 0x5;
-  int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), qp, 0xf, 0xf, false);
-  int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), qp, 0xf, 0xf, false);
-  lo = __builtin_amdgcn_update_dpp(lo, lo, sh, 0xf, bm, false);
-  hi = __builtin_amdgcn_update_dpp(hi, hi, sh, 0xf, bm, false);
-  return __hiloint2double(hi, lo);
-#else
-  constexpr int off = 0x18 | (K << 5);  // swizzle bitmask mode: and 0x18, or K
-  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), off);
-  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), off);
-  return __hiloint2double(hi, lo);
-#endif
 }
 // ROW: the group is lanes 0..7 of a 16-lane DPP row whose lanes 8..15 do
 // not take part (k_node's calc): one row_newbcast move per broadcast

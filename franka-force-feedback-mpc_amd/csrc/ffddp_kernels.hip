@@ -123,8 +123,10 @@ __device__ __forceinline__ long xcd_block(long b, long n) {
 // ---------------------------------------------------------------------------
 // init
 // ---------------------------------------------------------------------------
-__global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* __restrict__ xs_init,
-                       const double* __restrict__ us_init, int is_feasible) {
+// xs_init / us_init may be d.xs / d.us (warm start in place, ffddp.h): not
+// __restrict__; each element is read and written by the same thread
+__global__ void k_init(const DevConsts* __restrict__ Cg, Dev d, const double* xs_init, const double* us_init,
+                       int is_feasible) {
   const DevConsts& C = *Cg;
   const int N = C.N, nx = C.nx;
   const long nX = (long)d.B * (N + 1) * nx;
@@ -2301,9 +2303,8 @@ struct ProfScope {
   }
 };
 
-// profiling classes: one kernel per class (KC_COMMIT: the end-of-solve
-// k_commit; KC_PRIMAL is no longer launched: the calc runs inside k_node)
-enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE, KC_FORWARD2, KC_PRIMAL };
+// profiling classes: one kernel per class (KC_COMMIT: the end-of-solve k_commit)
+enum { KC_INIT = 0, KC_NODE, KC_BACKWARD, KC_FORWARD, KC_ACCEPT, KC_COMMIT, KC_FINALIZE, KC_FORWARD2 };
 
 // the per-instance slice [b0, b0 + Bk) of the handle workspace
 Dev dev_slice(const Dev& d0, int b0, int Bk, int k) {
@@ -2803,6 +2804,16 @@ int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double
                       cost, iters, ok, fn_pred, stats, (hipStream_t)stream);
 }
 
+// error exit of the host entry point after its first asynchronous copy: the
+// slice streams may still be copying from the staging buffer or the caller's
+// page-locked arrays, or into them; wait for all of them before returning
+static int drain_host_solve(ffddp_handle* h, int rc) {
+  for (hipStream_t st : h->streams) (void)hipStreamSynchronize(st);
+  (void)hipStreamSynchronize(nullptr);
+  (void)hipGetLastError();
+  return rc;
+}
+
 int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* node_ref, const double* inst_ref,
                       const uint8_t* surface, const double* xs_init, const double* us_init, int maxiter,
                       int is_feasible, double* xs, double* us, double* K, double* cost, int32_t* iters, uint8_t* ok,
@@ -2876,14 +2887,13 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
   int rc = launch_solve(h, B, h->in_x0, h->in_nref, h->in_iref, h->in_surf, h->in_xs, h->in_us, maxiter, is_feasible,
                         (double*)hout[0], (double*)hout[1], (double*)hout[2], h->out_cost, h->out_iters, h->out_ok,
                         h->out_fn, h->out_stats, cs, &io);
-  if (rc) {
-    (void)hipStreamSynchronize(cs);
-    return rc;
-  }
+  if (rc) return drain_host_solve(h, rc);
   const double t2 = tm ? now() : 0.0;
   double tw[8] = {0}, tc[8] = {0};
   for (int k = 0; k < io.ns; ++k) {
-    HIPCHK(h, hipEventSynchronize(io.done[k]));
+    const hipError_t e = hipEventSynchronize(io.done[k]);
+    if (e != hipSuccess)
+      return drain_host_solve(h, fail(h, FFDDP_E_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(e)));
     if (tm) tw[k] = now();
     jobs.clear();
     for (int i = 0; i < 8; ++i) {
@@ -2894,7 +2904,11 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
     host_copy(jobs);
     if (tm) tc[k] = now();
   }
-  HIPCHK(h, hipStreamSynchronize(cs));
+  {
+    const hipError_t e = hipStreamSynchronize(cs);
+    if (e != hipSuccess)
+      return drain_host_solve(h, fail(h, FFDDP_E_DEVICE, std::string("hipStreamSynchronize: ") + hipGetErrorString(e)));
+  }
   if (tm) {
     std::fprintf(stderr, "[ffddp host io] stage-in %.2f ms, enqueue %.2f ms", t1 - t0, t2 - t1);
     for (int k = 0; k < io.ns; ++k) std::fprintf(stderr, " | slice %d done +%.2f copied +%.2f", k, tw[k] - t0, tc[k] - t0);

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 from pathlib import Path
 
 import numpy as np
@@ -49,7 +50,7 @@ TRACE_W = 10
 TRACE_FIELDS = ("iter", "cost", "stop", "grad", "preg", "dreg", "step", "ffeas", "dV", "dV_exp")
 NEGSTEP_CROCODDYL = 0
 NEGSTEP_BOUNDED_RISE = 1
-KERNEL_CLASSES = ("init", "node", "backward", "forward", "accept", "commit", "finalize", "forward2", "primal")
+KERNEL_CLASSES = ("init", "node", "backward", "forward", "accept", "commit", "finalize", "forward2")
 
 
 class Robot(C.Structure):
@@ -328,27 +329,19 @@ def iptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_int32))
 
 
-class _PinnedBlock:
-    """One ffddp_host_alloc allocation; freed when the last array viewing it
-    is gone (every array's buffer keeps the block alive)."""
-
-    def __init__(self, nbytes: int):
-        self._lib = load()
-        p = C.c_void_p()
-        rc = self._lib.ffddp_host_alloc(max(int(nbytes), 1), C.byref(p))
-        if rc != 0:
-            raise MemoryError(f"ffddp_host_alloc({nbytes}) failed ({rc})")
-        self.ptr = p
-        self.buf = (C.c_char * max(int(nbytes), 1)).from_address(p.value)
-        self.buf._owner = self
-
-    def __del__(self):
-        try:
-            if self.ptr is not None and self.ptr.value:
-                self._lib.ffddp_host_free(self.ptr)
-                self.ptr = None
-        except Exception:
-            pass
+def _pinned_buffer(nbytes: int):
+    """One ffddp_host_alloc allocation as a ctypes buffer, freed (weakref
+    finalizer, no reference cycle) as soon as the buffer -- and so the last
+    numpy array viewing it -- is gone."""
+    lib = load()
+    n = max(int(nbytes), 1)
+    p = C.c_void_p()
+    rc = lib.ffddp_host_alloc(n, C.byref(p))
+    if rc != 0:
+        raise MemoryError(f"ffddp_host_alloc({nbytes}) failed ({rc})")
+    buf = (C.c_char * n).from_address(p.value)
+    weakref.finalize(buf, lib.ffddp_host_free, C.c_void_p(p.value))
+    return buf
 
 
 def pinned_arrays(specs) -> dict:
@@ -359,8 +352,8 @@ def pinned_arrays(specs) -> dict:
     for k, (shape, dt) in specs.items():
         offs[k] = tot
         tot += (int(np.prod(shape)) * np.dtype(dt).itemsize + 255) // 256 * 256
-    blk = _PinnedBlock(tot)
-    return {k: np.frombuffer(blk.buf, dtype=dt, count=int(np.prod(shape)), offset=offs[k]).reshape(shape)
+    buf = _pinned_buffer(tot)
+    return {k: np.frombuffer(buf, dtype=dt, count=int(np.prod(shape)), offset=offs[k]).reshape(shape)
             for k, (shape, dt) in specs.items()}
 
 

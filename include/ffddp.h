@@ -8,12 +8,17 @@
  * `solver` is crocoddyl.SolverBoxFDDP(problem) (crocoddyl_classical.py:442-445)
  * over the ShootingProblem built by _build_problem (:521-556 / FF :776-836).
  * The reference binds Crocoddyl through boost-python; this library is bound
- * through ctypes.  Plain pointers and sizes only.
+ * through ctypes (ffddp._abi) and through a pybind11 module over the same
+ * entry points (csrc/ffddp_pybind.cpp).  Plain pointers
+ * and sizes only.
  *
  * Conventions
  *   - fp64 everywhere; all matrices row-major.
  *   - One handle = one OCP definition (robot + weights + horizon + variant),
- *     bound to one HIP device.  A handle is not thread-safe.
+ *     bound to one HIP device.  A handle is not thread-safe.  Handles on the
+ *     same device share one pool of slice streams (and the null stream), so
+ *     solves of two handles driven from two threads are correct but
+ *     serialise on the GPU rather than overlap.
  *   - Return 0 on success or a negative FFDDP_E* code for API / launch / OOM
  *     errors.  Per-instance numerical failure is reported in ok[b] = 0 (the
  *     cost may be NaN), exactly like Crocoddyl's solve() returning False.
@@ -33,7 +38,7 @@ extern "C" {
 #define FFDDP_NU 7      /* ActuationModelFull: nu = nv (:147) */
 #define FFDDP_MAX_NC 3  /* ContactModel1D (nc=1) or ContactModel3D (nc=3) */
 #define FFDDP_NSTATS 10 /* per-instance counters returned by the solve */
-#define FFDDP_NKERNELS 9 /* kernel classes reported by ffddp_profile_read */
+#define FFDDP_NKERNELS 8 /* kernel classes reported by ffddp_profile_read */
 
 enum {
   FFDDP_OK = 0,
@@ -92,8 +97,10 @@ typedef struct ffddp_ocp_config {
   int32_t use_inner_state_reg, use_inner_tau_reg;
   /* friction cone, built only for nc = 3 (crocoddyl_classical.py:678-687; FF
    * crocoddyl_force_feedback.py:959-966): ResidualModelContactFrictionCone over
-   * crocoddyl.FrictionCone(I, mu, nf = 4, inner = False) (:1428-1446) with a
-   * QuadraticBarrier narrowed by friction_margin (:891-903), weight w_friction_cone */
+   * crocoddyl.FrictionCone(I, mu, nf = 4, inner = False)
+   * (crocoddyl_classical.py:999-1018, crocoddyl_force_feedback.py:1428-1447)
+   * with a QuadraticBarrier narrowed by friction_margin (:891-903), weight
+   * w_friction_cone */
   double w_friction_cone, mu;
 } ffddp_ocp_config;
 
@@ -241,14 +248,13 @@ int ffddp_host_free(void* p);
  * forward (line search, first pass), accept (acceptance test, regularisation,
  * stopping; no copy: the next node kernel reads the accepted trial in place),
  * commit (end of solve: accepted trials no node kernel consumed become
- * xs / us), finalize, forward2 (line search, second pass), primal (unused:
- * the calc runs inside the node kernel).
+ * xs / us), finalize, forward2 (line search, second pass).
  * `classes` is a bit mask over those classes (bit i = class i; 0 = off,
  * FFDDP_PROFILE_ALL = every class).  Timing only the kernel of interest keeps
  * the event overhead out of the other launches.
  * ffddp_profile_read synchronises the recorded events and returns, per class,
  * the summed milliseconds and launch counts since the last reset. */
-#define FFDDP_PROFILE_ALL 0x1FF
+#define FFDDP_PROFILE_ALL 0xFF
 int ffddp_profile_enable(ffddp_handle* h, int classes);
 int ffddp_profile_read(ffddp_handle* h, double* ms, int64_t* launches, int reset);
 

@@ -364,7 +364,8 @@ def dynamics_derivatives(cfg, q, v, dyn, surface, p_star):
 
 def friction_cone(cfg):
     """crocoddyl.FrictionCone(R=I, mu, nf=4, inner_appr=False) as the reference
-    builds it (crocoddyl_classical.py:1428-1446; Crocoddyl 2.x FrictionCone::update:
+    builds it (crocoddyl_classical.py:999-1018, crocoddyl_force_feedback.py:1428-1447;
+    Crocoddyl 2.x FrictionCone::update:
     facet rows (-mu e_z +- t_i)^T R^T with t_i = (cos th_i, sin th_i, 0),
     th_i = i 2 pi / nf, bounds (-inf, 0]; row nf = R e_z with bounds
     [min_nforce = 0, inf)), and the barrier bounds of

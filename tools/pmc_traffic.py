@@ -20,7 +20,7 @@ from pathlib import Path
 
 # kernel name -> bench/profiler class (ffddp_profile_read classes, one kernel each)
 CLASS_OF = (
-    ("k_primal", "primal"), ("k_node", "node"), ("k_backward", "backward"), ("k_forward", "forward"),
+    ("k_node", "node"), ("k_backward", "backward"), ("k_forward", "forward"),
     ("k_accept", "accept"), ("k_commit", "commit"), ("k_init", "init"), ("k_finalize", "finalize"),
 )
 SLICE_B = 1024  # instances per sub-batch slice (B / FFDDP_STREAMS)
