@@ -1,0 +1,75 @@
+"""Where a configs[0] closed-loop tick goes (flat scenario, one robot, HIP
+solver + HIP plant): per tick, the controller's wall time, the solve() call
+inside it (host entry point: staging, copies, launches, wait), and the
+solve's kernels (per-class HIP-event sums, ffddp_profile_read), plus the
+plant step.  Prints one JSON line.
+
+    python tools/c1_breakdown.py [--time 4] [--neg-step-rule 0]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import ffddp_path  # noqa: E402,F401
+import numpy as np  # noqa: E402
+
+from ffddp import closed_loop, controller as CT, solver as SV  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--time", type=float, default=4.0)
+    ap.add_argument("--neg-step-rule", type=int, default=0)
+    ap.add_argument("--profile", action="store_true", help="per-kernel HIP events (adds event overhead)")
+    a = ap.parse_args()
+    solve_s, iters, ctrl_s = [], [], []
+    orig_solve = SV.BatchedBoxFDDP.solve
+    orig_cc = CT.ClassicalCrocoddylMPC.compute_control
+    prof = {}
+
+    def solve(self, *args, **kw):
+        if a.profile and not getattr(self, "_prof_on", False):
+            self.profile(True)
+            self._prof_on = True
+        t0 = time.perf_counter()
+        r = orig_solve(self, *args, **kw)
+        solve_s.append(time.perf_counter() - t0)
+        iters.append(int(self.iter[0]))
+        if a.profile:
+            for k, (ms, n) in self.profile_read(reset=True).items():
+                p = prof.setdefault(k, [0.0, 0])
+                p[0] += ms
+                p[1] += n
+        return r
+
+    def cc(self, obs, t):
+        t0 = time.perf_counter()
+        r = orig_cc(self, obs, t)
+        ctrl_s.append(time.perf_counter() - t0)
+        return r
+
+    SV.BatchedBoxFDDP.solve = solve
+    CT.ClassicalCrocoddylMPC.compute_control = cc
+    s = closed_loop.run_single("flat", a.time, verbose=False, log=False, neg_step_rule=a.neg_step_rule)
+    n = len(solve_s)
+    skip = min(20, n // 4)  # first ticks: allocation, staging buffers
+    sl = slice(skip, None)
+    out = {"ticks": s["ticks"], "neg_step_rule": a.neg_step_rule, "wall_ms_per_tick": 1e3 * s["wall_s"] / s["ticks"],
+           "controller_ms": 1e3 * float(np.mean(ctrl_s[sl])), "solve_call_ms": 1e3 * float(np.mean(solve_s[sl])),
+           "solve_call_ms_p50": 1e3 * float(np.median(solve_s[sl])), "mean_iters": float(np.mean(iters[sl])),
+           "host_controller_ms": 1e3 * float(np.mean(np.array(ctrl_s[sl]) - np.array(solve_s[sl])))}
+    if a.profile:
+        out["kernels_ms_per_solve"] = {k: v[0] / n for k, v in prof.items() if v[1]}
+        out["launches_per_solve"] = {k: v[1] / n for k, v in prof.items() if v[1]}
+        out["kernel_ms_per_solve"] = sum(v[0] for v in prof.values()) / n
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,15 +1,27 @@
 #!/usr/bin/env python3
-"""Per-kernel-class sums of SQ counters from tools/pmc_sq2.sh passes."""
-import csv, sys
+"""Per-kernel SQ counters from tools/pmc_sq2.sh passes: sums and per-wave
+averages per kernel (template variants kept apart, e.g. the two backward
+variants), then the derived ratios per kernel.  SQ_WAVE_CYCLES, SQ_WAIT_* and
+SQ_ACTIVE_INST_* all count quad-cycles (MI355X_MICROARCH.md, PMC units), and
+WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES, so:
+  FMA share    SQ_INSTS_VALU_FMA_F64 / SQ_INSTS_VALU
+  VALU-active  SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
+  LDS-active   SQ_ACTIVE_INST_LDS / SQ_WAVE_CYCLES
+  waiting      SQ_WAIT_ANY / SQ_WAVE_CYCLES   (parked on s_waitcnt / barrier)
+  issue-stall  SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
+  bank conflicts per wave  SQ_LDS_BANK_CONFLICT / SQ_WAVES
+Per-wave averages include waves that exit at once (grid slots past the active
+count), so per-wave figures are lower bounds of a working wave's."""
+import csv
+import re
+import sys
 from collections import defaultdict
 from pathlib import Path
 
-import re
-
 
 def kclass(n):
-    m = re.search(r"k_[a-z0-9_]+", n)
-    return m.group(0)[2:] if m else None
+    m = re.search(r"k_[a-z0-9_]+(<[^>(]*>)?", n)
+    return m.group(0)[2:].replace(" ", "") if m else None
 
 
 tot = defaultdict(lambda: defaultdict(float))
@@ -23,7 +35,19 @@ busy = 0.0
 for c, d in tot.items():
     busy += d.get("SQ_ACTIVE_INST_VALU", 0.0) * 4
 print(f"VALU-active cycles (all kernels): {busy:.4g}  = {busy / 1024 / 2.4e9 * 1e3:.3f} ms of all 1024 SIMDs at 2.4 GHz")
-for c, d in tot.items():
+print()
+print(f"{'kernel':34s} {'waves':>8s} {'FMA/VALU':>9s} {'VALU-act':>9s} {'LDS-act':>8s} {'waiting':>8s} "
+      f"{'issue-st':>8s} {'bankconf/w':>10s} {'VALU/w':>8s} {'cyc/w':>8s}")
+for c, d in sorted(tot.items()):
+    w = d.get("SQ_WAVES", 0) or 1
+    wc = d.get("SQ_WAVE_CYCLES", 0) or 1
+    r = lambda k: d.get(k, 0.0) / wc  # noqa: E731
+    fma = d.get("SQ_INSTS_VALU_FMA_F64", 0.0) / (d.get("SQ_INSTS_VALU", 0.0) or 1)
+    print(f"{c:34s} {w:8.0f} {fma:9.1%} {r('SQ_ACTIVE_INST_VALU'):9.1%} {r('SQ_ACTIVE_INST_LDS'):8.1%} "
+          f"{r('SQ_WAIT_ANY'):8.1%} {r('SQ_WAIT_INST_ANY'):8.1%} {d.get('SQ_LDS_BANK_CONFLICT', 0) / w:10.1f} "
+          f"{d.get('SQ_INSTS_VALU', 0) / w:8.0f} {4 * wc / w:8.0f}")
+print()
+for c, d in sorted(tot.items()):
     w = d.get("SQ_WAVES", 0) or 1
     print(f"== {c}: waves {w:.0f}")
     for k in sorted(d):
