@@ -2917,6 +2917,164 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// solve plans: the whole host-array solve of a fixed batch captured once as a
+// HIP graph (one input copy, every kernel, one output copy) and replayed per
+// call -- the receding-horizon loop's one solve per control tick
+// ---------------------------------------------------------------------------
+struct ffddp_plan {
+  ffddp_handle* h = nullptr;
+  int B = 0;
+  hipStream_t s = nullptr;
+  hipGraphExec_t ge = nullptr;
+  char *hin = nullptr, *hout = nullptr;  // page-locked, packed
+  char *din = nullptr, *dout = nullptr;  // device, same layouts
+  size_t in_bytes = 0, out_bytes = 0;
+};
+
+namespace {
+// packed layouts: 8-byte fields first, then int32, then bytes; each field
+// starts on a 256-byte boundary
+struct PlanLayout {
+  size_t x0, nref, iref, xs_init, us_init, surf, in_bytes;
+  size_t xs, us, K, cost, fn, iters, stats, ok, out_bytes;
+};
+static PlanLayout plan_layout(int B, int N, int nx) {
+  PlanLayout L{};
+  size_t o = 0;
+  auto put = [&](size_t bytes) {
+    const size_t at = o;
+    o += (bytes + 255) / 256 * 256;
+    return at;
+  };
+  const size_t b = (size_t)B, n = (size_t)N, x = (size_t)nx;
+  L.x0 = put(b * x * 8);
+  L.nref = put(b * (n + 1) * 6 * 8);
+  L.iref = put(b * 21 * 8);
+  L.xs_init = put(b * (n + 1) * x * 8);
+  L.us_init = put(b * n * NU * 8);
+  L.surf = put(b);
+  L.in_bytes = o;
+  o = 0;
+  L.xs = put(b * (n + 1) * x * 8);
+  L.us = put(b * n * NU * 8);
+  L.K = put(b * n * NU * x * 8);
+  L.cost = put(b * 8);
+  L.fn = put(b * 2 * 8);
+  L.iters = put(b * 4);
+  L.stats = put(b * FFDDP_NSTATS * 4);
+  L.ok = put(b);
+  L.out_bytes = o;
+  return L;
+}
+
+static void plan_free(ffddp_plan* p) {
+  if (p->ge) (void)hipGraphExecDestroy(p->ge);
+  if (p->s) (void)hipStreamDestroy(p->s);
+  if (p->din) (void)hipFree(p->din);
+  if (p->dout) (void)hipFree(p->dout);
+  if (p->hin) (void)hipHostFree(p->hin);
+  if (p->hout) (void)hipHostFree(p->hout);
+  delete p;
+}
+}  // namespace
+
+int ffddp_plan_create(ffddp_handle* h, int B, int maxiter, int is_feasible, ffddp_plan** out, ffddp_plan_io* io) {
+  if (!h) return FFDDP_E_INVALID;
+  if (!out || !io) return fail(h, FFDDP_E_INVALID, "null pointer");
+  *out = nullptr;
+  if (B < 1 || maxiter < 0) return fail(h, FFDDP_E_INVALID, "plan needs B >= 1 and maxiter >= 0");
+  if (B > h->max_batch) return fail(h, FFDDP_E_CAPACITY, "B exceeds max_batch");
+  HIPCHK(h, hipSetDevice(h->device));
+  const int N = h->hc.N, nx = h->hc.nx;
+  const PlanLayout L = plan_layout(B, N, nx);
+  ffddp_plan* p = new (std::nothrow) ffddp_plan();
+  if (!p) return fail(h, FFDDP_E_OOM, "plan allocation failed");
+  p->h = h;
+  p->B = B;
+  p->in_bytes = L.in_bytes;
+  p->out_bytes = L.out_bytes;
+  if (hipHostMalloc((void**)&p->hin, L.in_bytes, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&p->hout, L.out_bytes, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc((void**)&p->din, L.in_bytes) != hipSuccess || hipMalloc((void**)&p->dout, L.out_bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    plan_free(p);
+    return fail(h, FFDDP_E_OOM, "plan buffers");
+  }
+  std::memset(p->hin, 0, L.in_bytes);
+  std::memset(p->hout, 0, L.out_bytes);
+  if (hipStreamCreateWithFlags(&p->s, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    plan_free(p);
+    return fail(h, FFDDP_E_DEVICE, "hipStreamCreate (plan)");
+  }
+  // capture: inputs up, the device entry point's launch sequence iterating in
+  // the plan's own output region, outputs down.  Per-kernel timing events are
+  // not captured (profiling is off while capturing).
+  const bool prof = h->prof;
+  h->prof = false;
+  char* di = p->din;
+  char* dq = p->dout;
+  int rc = 0;
+  hipError_t e = hipStreamBeginCapture(p->s, hipStreamCaptureModeThreadLocal);
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(p->din, p->hin, L.in_bytes, hipMemcpyHostToDevice, p->s);
+    if (e == hipSuccess)
+      rc = launch_solve(h, B, (const double*)(di + L.x0), (const double*)(di + L.nref), (const double*)(di + L.iref),
+                        (const uint8_t*)(di + L.surf), (const double*)(di + L.xs_init),
+                        (const double*)(di + L.us_init), maxiter, is_feasible, (double*)(dq + L.xs),
+                        (double*)(dq + L.us), (double*)(dq + L.K), (double*)(dq + L.cost), (int32_t*)(dq + L.iters),
+                        (uint8_t*)(dq + L.ok), (double*)(dq + L.fn), (int32_t*)(dq + L.stats), p->s);
+    if (e == hipSuccess && rc == 0) e = hipMemcpyAsync(p->hout, p->dout, L.out_bytes, hipMemcpyDeviceToHost, p->s);
+    hipGraph_t g = nullptr;
+    const hipError_t e2 = hipStreamEndCapture(p->s, &g);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess && rc == 0) e = hipGraphInstantiate(&p->ge, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+  }
+  h->prof = prof;
+  if (rc == 0 && e != hipSuccess) rc = fail(h, FFDDP_E_DEVICE, std::string("plan capture: ") + hipGetErrorString(e));
+  if (rc) {
+    (void)hipGetLastError();
+    plan_free(p);
+    return rc;
+  }
+  char* hi = p->hin;
+  char* ho = p->hout;
+  io->x0 = (double*)(hi + L.x0);
+  io->node_ref = (double*)(hi + L.nref);
+  io->inst_ref = (double*)(hi + L.iref);
+  io->surface = (uint8_t*)(hi + L.surf);
+  io->xs_init = (double*)(hi + L.xs_init);
+  io->us_init = (double*)(hi + L.us_init);
+  io->xs = (const double*)(ho + L.xs);
+  io->us = (const double*)(ho + L.us);
+  io->K = (const double*)(ho + L.K);
+  io->cost = (const double*)(ho + L.cost);
+  io->iters = (const int32_t*)(ho + L.iters);
+  io->ok = (const uint8_t*)(ho + L.ok);
+  io->fn_pred = (const double*)(ho + L.fn);
+  io->stats = (const int32_t*)(ho + L.stats);
+  *out = p;
+  return 0;
+}
+
+int ffddp_plan_run(ffddp_plan* p) {
+  if (!p) return FFDDP_E_INVALID;
+  ffddp_handle* h = p->h;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipGraphLaunch(p->ge, p->s));
+  HIPCHK(h, hipStreamSynchronize(p->s));
+  return 0;
+}
+
+void ffddp_plan_destroy(ffddp_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->h->device);
+  (void)hipStreamSynchronize(p->s);
+  plan_free(p);
+}
+
 int ffddp_host_alloc(size_t bytes, void** p) {
   if (!p) return FFDDP_E_INVALID;
   *p = nullptr;

@@ -43,6 +43,9 @@ SYMBOLS = (
     "ffddp_trace_read",
     "ffddp_host_alloc",
     "ffddp_host_free",
+    "ffddp_plan_create",
+    "ffddp_plan_run",
+    "ffddp_plan_destroy",
 )
 PLANT_OBS = 69
 NSTATS = 10
@@ -111,6 +114,13 @@ class OcpConfig(C.Structure):
         ("w_friction_cone", C.c_double),
         ("mu", C.c_double),
     ]
+
+
+class PlanIO(C.Structure):
+    """ffddp_plan_io (include/ffddp.h): the plan's page-locked inputs / outputs."""
+
+    _fields_ = [(n, C.c_void_p) for n in ("x0", "node_ref", "inst_ref", "surface", "xs_init", "us_init", "xs", "us",
+                                          "K", "cost", "iters", "ok", "fn_pred", "stats")]
 
 
 class SolverParams(C.Structure):
@@ -315,6 +325,12 @@ def load() -> C.CDLL:
     lib.ffddp_host_alloc.restype = C.c_int
     lib.ffddp_host_free.argtypes = [C.c_void_p]
     lib.ffddp_host_free.restype = C.c_int
+    lib.ffddp_plan_create.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(PlanIO)]
+    lib.ffddp_plan_create.restype = C.c_int
+    lib.ffddp_plan_run.argtypes = [C.c_void_p]
+    lib.ffddp_plan_run.restype = C.c_int
+    lib.ffddp_plan_destroy.argtypes = [C.c_void_p]
+    lib.ffddp_plan_destroy.restype = None
     _lib = lib
     return lib
 

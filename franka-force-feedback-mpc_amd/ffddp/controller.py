@@ -198,7 +198,10 @@ def _quat_wxyz_to_R(q) -> np.ndarray:
 class _MPCBase:
     variant = "classical"
 
-    def __init__(self, sim, traj_fn: Traj, config, device: int = 0):
+    def __init__(self, sim, traj_fn: Traj, config, device: int = 0, use_plan: bool = True):
+        """use_plan: run each tick's solve through a captured solve plan
+        (BatchedBoxFDDP.plan: one graph launch per tick, bit-identical to
+        solve()); False: the plain host-array solve."""
         cfg = config
         self.sim = sim
         self.traj_fn = traj_fn
@@ -231,6 +234,9 @@ class _MPCBase:
         self.ocp = self._ocp_config()
         self._solver = BatchedBoxFDDP(self.ocp, max_batch=1, device=device)
         self._solver.neg_step_rule = int(getattr(self.cfg, "neg_step_rule", 0))
+        self._use_plan = bool(use_plan) and hasattr(self._solver, "plan")
+        self._plan = None
+        self._res = self._solver  # where the last solve's outputs live (solver or plan)
         if self.cfg.verbose:  # crocoddyl_classical.py:352-353, 360-361
             self._solver.setCallbacks([CallbackVerbose()], max_iters=max(int(self.cfg.max_iters), 1))
 
@@ -370,8 +376,16 @@ class _MPCBase:
         prob = self._problem_arrays(t, x0, surface_now)
         xs_init, us_init = self._shift_guess(x0, N)
         s = self._solver
-        ok = bool(s.solve(prob, maxiter=int(self.cfg.max_iters), is_feasible=False,
-                          xs_init=np.asarray(xs_init)[None], us_init=np.asarray(us_init)[None])[0])
+        if self._use_plan:
+            if self._plan is None:
+                self._plan = s.plan(1, maxiter=int(self.cfg.max_iters), is_feasible=False)
+            s = self._plan
+            s.fill(prob, xs_init=np.asarray(xs_init)[None], us_init=np.asarray(us_init)[None])
+            ok = bool(s.run()[0])
+        else:
+            ok = bool(s.solve(prob, maxiter=int(self.cfg.max_iters), is_feasible=False,
+                              xs_init=np.asarray(xs_init)[None], us_init=np.asarray(us_init)[None])[0])
+        self._res = s
         cost, iters = float(s.cost[0]), int(s.iter[0])
         st = getattr(s, "stats", None)
         # ascent-direction branch (dVexp < 0): trials judged / accepted in this solve
@@ -408,6 +422,9 @@ class _MPCBase:
             self._prev_surface_mode = bool(surface_now)
 
     def close(self):
+        if self._plan is not None:
+            self._plan.close()
+            self._plan = None
         self._solver.close()
 
 
@@ -416,8 +433,9 @@ class ClassicalCrocoddylMPC(_MPCBase):
 
     variant = "classical"
 
-    def __init__(self, sim, traj_fn: Traj, config: Optional[ClassicalMPCConfig] = None, device: int = 0):
-        super().__init__(sim, traj_fn, config if config is not None else ClassicalMPCConfig(), device)
+    def __init__(self, sim, traj_fn: Traj, config: Optional[ClassicalMPCConfig] = None, device: int = 0,
+                 use_plan: bool = True):
+        super().__init__(sim, traj_fn, config if config is not None else ClassicalMPCConfig(), device, use_plan)
 
     def _initial_tau(self, obs0):
         return obs0.tau_bias
@@ -448,7 +466,7 @@ class ClassicalCrocoddylMPC(_MPCBase):
         if self._need_solve():
             ok, cost, iters = self._solve(t, x0, surface_now)
             # _extract_predicted_normal_force: world-z contact force at knot 0 (R7)
-            fn_pred = float(self._solver.fn_pred[0, 0]) if surface_now else np.nan
+            fn_pred = float(self._res.fn_pred[0, 0]) if surface_now else np.nan
             solved_now = True
         tau_raw, policy_idx = self._policy_control(x0)
         tau_raw_inf = float(np.max(np.abs(tau_raw)))
@@ -485,12 +503,13 @@ class ForceFeedbackCrocoddylMPC(_MPCBase):
 
     variant = "ff"
 
-    def __init__(self, sim, traj_fn: Traj, config: Optional[ForceFeedbackMPCConfig] = None, device: int = 0):
+    def __init__(self, sim, traj_fn: Traj, config: Optional[ForceFeedbackMPCConfig] = None, device: int = 0,
+                 use_plan: bool = True):
         self.nx_aug = 21
         self._fn_pred_hist_raw: list = []
         self._fn_pred_hist_meas: list = []
         self._fn_pred_corr = np.nan
-        super().__init__(sim, traj_fn, config if config is not None else ForceFeedbackMPCConfig(), device)
+        super().__init__(sim, traj_fn, config if config is not None else ForceFeedbackMPCConfig(), device, use_plan)
 
     def _initial_tau(self, obs0):
         return obs0.tau_cmd
@@ -592,10 +611,10 @@ class ForceFeedbackCrocoddylMPC(_MPCBase):
     # -- force prediction (crocoddyl_force_feedback.py:1219-1243, 1301-1371) ----------
     def _predicted_normal_force_next_step(self) -> float:
         N = int(self.cfg.horizon)
-        f0 = abs(float(self._solver.fn_pred[0, 0]))
+        f0 = abs(float(self._res.fn_pred[0, 0]))
         if N == 1:
             return f0
-        f1 = abs(float(self._solver.fn_pred[0, 1]))
+        f1 = abs(float(self._res.fn_pred[0, 1]))
         if not np.isfinite(f0):
             return f1
         if not np.isfinite(f1):

@@ -182,6 +182,12 @@ class BatchedBoxFDDP:
         self._run_callbacks(B)
         return self.ok
 
+    # -- solve plan (receding-horizon loop: one graph launch per tick) -----------------
+    def plan(self, B: int, maxiter: int = 10, is_feasible: bool = False) -> "SolvePlan":
+        """ffddp_plan_create: the host-array solve of B instances captured as one
+        HIP graph; see SolvePlan."""
+        return SolvePlan(self, B, maxiter, is_feasible)
+
     # -- solve (device-resident torch tensors; bench path) ---------------------------
     def solve_dev(self, t, maxiter: int = 10, is_feasible: bool = False, stream=None):
         """t: dict of contiguous torch.cuda tensors with keys x0, node_ref, inst_ref,
@@ -253,3 +259,76 @@ class BatchedBoxFDDP:
         )
         self._check(rc, "ffddp_calc_diff")
         return out
+
+
+class SolvePlan:
+    """A captured solve of a fixed batch (include/ffddp.h ffddp_plan_*): the
+    per-tick solve of a receding-horizon loop (crocoddyl_classical.py:367,
+    run_classical.py:412) as one graph launch -- inputs up, every kernel,
+    outputs down.  Fill the input views (x0, node_ref, inst_ref, surface,
+    xs_init, us_init: page-locked numpy arrays owned by the plan) in place,
+    call run(); the output views (xs, us, K, cost, iter, ok, fn_pred, stats)
+    hold the last run's solution and are overwritten by the next run, so copy
+    what must outlive it.  Same results as BatchedBoxFDDP.solve, bit for bit."""
+
+    def __init__(self, solver: BatchedBoxFDDP, B: int, maxiter: int, is_feasible: bool):
+        self.solver, self.B, self.maxiter = solver, int(B), int(maxiter)
+        lib = solver._lib
+        io = _abi.PlanIO()
+        h = C.c_void_p()
+        solver._check(lib.ffddp_plan_create(solver._h, self.B, self.maxiter, int(bool(is_feasible)), C.byref(h),
+                                            C.byref(io)), "ffddp_plan_create")
+        self._h, self._lib = h, lib
+        B, N, nx = self.B, solver.N, solver.nx
+
+        def view(ptr, shape, ct, dt):
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=shape).view(dt)
+
+        f, i32, u8 = C.c_double, C.c_int32, C.c_uint8
+        self.x0 = view(io.x0, (B, nx), f, np.float64)
+        self.node_ref = view(io.node_ref, (B, N + 1, 6), f, np.float64)
+        self.inst_ref = view(io.inst_ref, (B, 21), f, np.float64)
+        self.surface = view(io.surface, (B,), u8, np.uint8)
+        self.xs_init = view(io.xs_init, (B, N + 1, nx), f, np.float64)
+        self.us_init = view(io.us_init, (B, N, 7), f, np.float64)
+        self.xs = view(io.xs, (B, N + 1, nx), f, np.float64)
+        self.us = view(io.us, (B, N, 7), f, np.float64)
+        self.K = view(io.K, (B, N, 7, nx), f, np.float64)
+        self.cost = view(io.cost, (B,), f, np.float64)
+        self.iter = view(io.iters, (B,), i32, np.int32)
+        self._ok = view(io.ok, (B,), u8, np.uint8)
+        self.fn_pred = view(io.fn_pred, (B, 2), f, np.float64)
+        self.stats = view(io.stats, (B, _abi.NSTATS), i32, np.int32)
+
+    @property
+    def ok(self) -> np.ndarray:
+        return self._ok.astype(bool)
+
+    def fill(self, batch, xs_init=None, us_init=None):
+        """Copy a workload.Batch (and optional warm start) into the input views."""
+        self.x0[...] = np.asarray(batch.x0, np.float64).reshape(self.x0.shape)
+        self.node_ref[...] = np.asarray(batch.node_ref, np.float64).reshape(self.node_ref.shape)
+        self.inst_ref[...] = np.asarray(batch.inst_ref, np.float64).reshape(self.inst_ref.shape)
+        self.surface[...] = np.asarray(batch.surface, np.uint8).reshape(self.surface.shape)
+        self.xs_init[...] = np.asarray(batch.xs_init if xs_init is None else xs_init, np.float64).reshape(
+            self.xs_init.shape)
+        self.us_init[...] = np.asarray(batch.us_init if us_init is None else us_init, np.float64).reshape(
+            self.us_init.shape)
+
+    def run(self) -> np.ndarray:
+        if self._h is None:
+            raise FfddpError("plan closed")
+        self.solver._check(self._lib.ffddp_plan_run(self._h), "ffddp_plan_run")
+        self.solver._run_callbacks(self.B)
+        return self.ok
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.ffddp_plan_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

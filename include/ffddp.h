@@ -173,6 +173,41 @@ int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double
                           double* us, double* K, double* cost, int32_t* iters, uint8_t* ok,
                           double* fn_pred, int32_t* stats, void* stream);
 
+/* Solve plan for a receding-horizon loop: one solve of a fixed batch per
+ * control tick (crocoddyl_classical.py:367 called every tick at
+ * run_classical.py:412).  ffddp_plan_create captures the whole host-array
+ * solve once as a HIP graph -- one copy of the packed inputs up, every kernel
+ * of maxiter iterations, one copy of the packed outputs down -- and
+ * ffddp_plan_run replays it and waits: one graph launch per tick instead of
+ * ~50 kernel launches and 14 copies.  The plan owns page-locked input and
+ * output arrays (the ffddp_solve_batch arguments, same layouts), returned in
+ * *io: refill the inputs in place before each run, read the outputs after it
+ * (overwritten by the next run).  Results equal ffddp_solve_batch's bit for
+ * bit.  The solver properties (ffddp_set_solver_params) apply to later runs;
+ * tracing and per-kernel timing are fixed at creation (timing off).  A plan
+ * uses its handle's workspace: destroy plans before their handle, and do not
+ * run a plan concurrently with another solve of the same handle. */
+typedef struct ffddp_plan ffddp_plan;
+typedef struct ffddp_plan_io {
+  double* x0;        /* [B][nx]        inputs, written by the caller */
+  double* node_ref;  /* [B][N+1][6] */
+  double* inst_ref;  /* [B][21] */
+  uint8_t* surface;  /* [B] */
+  double* xs_init;   /* [B][N+1][nx] */
+  double* us_init;   /* [B][N][7] */
+  const double* xs;  /* [B][N+1][nx]  outputs of the last run */
+  const double* us;  /* [B][N][7] */
+  const double* K;   /* [B][N][7][nx] */
+  const double* cost;
+  const int32_t* iters;
+  const uint8_t* ok;
+  const double* fn_pred; /* [B][2] */
+  const int32_t* stats;  /* [B][FFDDP_NSTATS] */
+} ffddp_plan_io;
+int ffddp_plan_create(ffddp_handle* h, int B, int maxiter, int is_feasible, ffddp_plan** out, ffddp_plan_io* io);
+int ffddp_plan_run(ffddp_plan* p);
+void ffddp_plan_destroy(ffddp_plan* p);
+
 /* problem.calcDiff(xs, us) on the device (ShootingProblem::calcDiff; used by
  * parity tests of the per-node models).  Host pointers.  Outputs per node in
  * Crocoddyl layout (running nodes t < N, terminal node t = N):

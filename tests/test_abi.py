@@ -41,6 +41,8 @@ int main(void) {
   printf("%zu %zu %zu %d %d %d ", sizeof(ffddp_solver_params), offsetof(ffddp_solver_params, reg_decfactor),
          offsetof(ffddp_solver_params, neg_step_rule), FFDDP_TRACE_W, FFDDP_NEGSTEP_CROCODDYL,
          FFDDP_NEGSTEP_BOUNDED_RISE);
+  printf("%zu %zu %zu %d %d ", sizeof(ffddp_plan_io), offsetof(ffddp_plan_io, xs), offsetof(ffddp_plan_io, stats),
+         FFDDP_NSTATS, FFDDP_NKERNELS);
   printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(ffddp_robot), sizeof(ffddp_ocp_config),
          offsetof(ffddp_ocp_config, dt), offsetof(ffddp_ocp_config, R_des),
          offsetof(ffddp_ocp_config, y_weights), offsetof(ffddp_ocp_config, use_inner_tau_reg),
@@ -63,6 +65,9 @@ int main(void) {
                         _abi.NEGSTEP_CROCODDYL, _abi.NEGSTEP_BOUNDED_RISE]
     assert len(_abi.TRACE_FIELDS) == _abi.TRACE_W
     vals = vals[6:]
+    Pio = _abi.PlanIO
+    assert vals[:5] == [ctypes.sizeof(Pio), Pio.xs.offset, Pio.stats.offset, _abi.NSTATS, len(_abi.KERNEL_CLASSES)]
+    vals = vals[5:]
     assert vals == [
         ctypes.sizeof(_abi.Robot), ctypes.sizeof(C), C.dt.offset, C.R_des.offset, C.y_weights.offset,
         C.use_inner_tau_reg.offset, ctypes.sizeof(_abi.Task), _abi.Task.has_ee_start.offset, _abi.Task.q_nom.offset,
@@ -105,6 +110,9 @@ def test_null_handle_errors():
     assert lib.ffddp_trace_read(None, 1, None) == -1
     assert lib.ffddp_host_alloc(16, None) == -1
     assert lib.ffddp_host_free(None) == 0
+    assert lib.ffddp_plan_create(None, 1, 10, 0, None, None) == -1
+    assert lib.ffddp_plan_run(None) == -1
+    lib.ffddp_plan_destroy(None)
 
 
 def test_solver_param_defaults_match_oracle():

@@ -1,10 +1,11 @@
 """Where a configs[0] closed-loop tick goes (flat scenario, one robot, HIP
 solver + HIP plant): per tick, the controller's wall time, the solve() call
-inside it (host entry point: staging, copies, launches, wait), and the
-solve's kernels (per-class HIP-event sums, ffddp_profile_read), plus the
-plant step.  Prints one JSON line.
+inside it (the solve plan's graph launch and wait, or with --no-plan the host
+entry point: staging, copies, launches, wait), and the
+solve's kernels (per-class HIP-event sums, ffddp_profile_read).  Prints one
+JSON line.
 
-    python tools/c1_breakdown.py [--time 4] [--neg-step-rule 0]
+    python tools/c1_breakdown.py [--time 4] [--neg-step-rule 0] [--no-plan | --profile]
 """
 from __future__ import annotations
 
@@ -26,10 +27,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--time", type=float, default=4.0)
     ap.add_argument("--neg-step-rule", type=int, default=0)
-    ap.add_argument("--profile", action="store_true", help="per-kernel HIP events (adds event overhead)")
+    ap.add_argument("--profile", action="store_true", help="per-kernel HIP events (adds event overhead; host-array"
+                    " solve only: a plan captures no timing events)")
+    ap.add_argument("--no-plan", action="store_true", help="plain host-array solve instead of the solve plan")
     a = ap.parse_args()
     solve_s, iters, ctrl_s = [], [], []
     orig_solve = SV.BatchedBoxFDDP.solve
+    orig_run = SV.SolvePlan.run
     orig_cc = CT.ClassicalCrocoddylMPC.compute_control
     prof = {}
 
@@ -48,6 +52,13 @@ def main():
                 p[1] += n
         return r
 
+    def run(self):
+        t0 = time.perf_counter()
+        r = orig_run(self)
+        solve_s.append(time.perf_counter() - t0)
+        iters.append(int(self.iter[0]))
+        return r
+
     def cc(self, obs, t):
         t0 = time.perf_counter()
         r = orig_cc(self, obs, t)
@@ -55,12 +66,17 @@ def main():
         return r
 
     SV.BatchedBoxFDDP.solve = solve
+    SV.SolvePlan.run = run
     CT.ClassicalCrocoddylMPC.compute_control = cc
+    if a.no_plan or a.profile:
+        init = CT.ClassicalCrocoddylMPC.__init__
+        CT.ClassicalCrocoddylMPC.__init__ = lambda self, *args, **kw: init(self, *args, **{**kw, "use_plan": False})
     s = closed_loop.run_single("flat", a.time, verbose=False, log=False, neg_step_rule=a.neg_step_rule)
     n = len(solve_s)
     skip = min(20, n // 4)  # first ticks: allocation, staging buffers
     sl = slice(skip, None)
-    out = {"ticks": s["ticks"], "neg_step_rule": a.neg_step_rule, "wall_ms_per_tick": 1e3 * s["wall_s"] / s["ticks"],
+    out = {"ticks": s["ticks"], "neg_step_rule": a.neg_step_rule, "plan": not (a.no_plan or a.profile),
+           "wall_ms_per_tick": 1e3 * s["wall_s"] / s["ticks"],
            "controller_ms": 1e3 * float(np.mean(ctrl_s[sl])), "solve_call_ms": 1e3 * float(np.mean(solve_s[sl])),
            "solve_call_ms_p50": 1e3 * float(np.median(solve_s[sl])), "mean_iters": float(np.mean(iters[sl])),
            "host_controller_ms": 1e3 * float(np.mean(np.array(ctrl_s[sl]) - np.array(solve_s[sl])))}
