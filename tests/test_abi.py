@@ -151,3 +151,18 @@ def test_integration_snippet_matches_header():
             "const uint8_t*": ns["U8"], "uint8_t*": ns["U8"], "int32_t*": ns["I32"]}
     params = [" ".join(p.split()[:-1]).replace(" *", "*") for p in proto.replace("\n", " ").split(",")]
     assert [cmap[p] for p in params] == doc_types
+
+
+def test_integration_plan_snippet_matches_header():
+    """INTEGRATION.md's solve-plan binding: the PlanIO fields are
+    ffddp_plan_io's, in order, and the create call's argtypes follow the
+    prototype."""
+    doc = (ROOT / "INTEGRATION.md").read_text()
+    block = doc.split("### One graph launch per tick")[1].split("```python")[1].split("```")[0]
+    hdr = HEADER.read_text()
+    body = re.search(r"typedef struct ffddp_plan_io \{(.*?)\} ffddp_plan_io;", hdr, re.S).group(1)
+    fields = re.findall(r"\*\s*(\w+);", body)
+    doc_fields = re.findall(r'"(\w+)"', re.search(r"_fields_ = \[(.*?)\]\n", block, re.S).group(1))
+    assert fields == doc_fields == [n for n, _ in _abi.PlanIO._fields_]
+    proto = re.search(r"int ffddp_plan_create\((.*?)\);", hdr, re.S).group(1)
+    assert len(proto.split(",")) == 6 and "lib.ffddp_plan_create.argtypes" in block
