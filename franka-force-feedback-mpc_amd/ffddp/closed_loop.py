@@ -25,7 +25,7 @@ import numpy as np
 from . import controller as CT
 from .plant import PandaTablePlant
 from .runlog import RunLogger, summary_metrics
-from .trajectory import TABLE_CENTER, TABLE_HALF_Z, TOOL_RADIUS, make_approach_then_circle
+from .trajectory import TABLE_CENTER, TABLE_HALF_Z, TOOL_RADIUS, make_approach_then_circle, with_contact_hold
 from .uncertainty import ScenarioUncertaintyInjector, config_for_scenario
 
 SCENARIOS = ("flat", "tilted_5", "tilted_10", "tilted_15", "actuation_uncertainty")
@@ -73,11 +73,7 @@ def run_single(scenario: str = "flat", total_time: float = 20.0, variant: str = 
                                      ee_start=obs.ee_pos.copy(), t_pre=t_pre)
     t_contact_phase = float(t_pre + t_approach)
 
-    def traj(tq: float):
-        p, v, s = base(tq)
-        if s and float(tq) < t_contact_phase + t_stab:
-            return np.asarray(base(t_contact_phase)[0], float), np.zeros(3), True
-        return p, v, s
+    traj = with_contact_hold(base, t_contact_phase, t_stab)
 
     max_iters = int(mpc_iters) if mpc_iters is not None else 10
     if variant == "ff":

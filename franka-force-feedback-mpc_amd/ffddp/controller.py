@@ -301,10 +301,19 @@ class _MPCBase:
         action models, as flat arrays: knot k uses traj(t0 + k dt_ocp)."""
         N, dt = int(self.cfg.horizon), self._dt_ocp
         node_ref = np.zeros((1, N + 1, 6))
-        for k in range(N + 1):
-            p, v, _ = self.traj_fn(t0 + k * dt)
-            node_ref[0, k, :3] = self._pos_mj_to_pin(p)
-            node_ref[0, k, 3:] = self._vel_mj_to_pin(v)
+        sample = getattr(self.traj_fn, "sample", None)
+        if sample is not None:
+            # all knots at once (trajectory.sample: the same arithmetic per
+            # knot; R_MJ_FROM_PIN is a signed permutation, so the frame maps
+            # below are exact in either order)
+            P, V, _ = sample(np.array([t0 + k * dt for k in range(N + 1)]))
+            node_ref[0, :, :3] = P @ self.R_mj_from_pin - self.p_site_minus_frame_pin
+            node_ref[0, :, 3:] = V @ self.R_mj_from_pin
+        else:
+            for k in range(N + 1):
+                p, v, _ = self.traj_fn(t0 + k * dt)
+                node_ref[0, k, :3] = self._pos_mj_to_pin(p)
+                node_ref[0, k, 3:] = self._vel_mj_to_pin(v)
         inst = np.concatenate([self._compute_posture_reference(x0), self._compute_tau_reference(x0[:7])])
         return Batch(x0[None].copy(), node_ref, inst[None], np.array([1 if surface_now else 0], np.uint8),
                      None, None, np.array([t0]))

@@ -34,7 +34,7 @@ from .controller import _OCP_FIELDS, _quat_wxyz_to_R, classical_benchmark_config
 from .plant import BatchedPlant, PandaTablePlant, observation_from_record
 from .runlog import summary_metrics
 from .solver import BatchedBoxFDDP
-from .trajectory import TABLE_CENTER, TABLE_HALF_Z, TOOL_RADIUS, make_approach_then_circle
+from .trajectory import TABLE_CENTER, TABLE_HALF_Z, TOOL_RADIUS, make_approach_then_circle, with_contact_hold
 from .uncertainty import ScenarioUncertaintyInjector, config_for_scenario
 
 Traj = Callable[[float], Tuple[np.ndarray, np.ndarray, bool]]
@@ -114,6 +114,12 @@ class FleetClassicalMPC:
 
     def _node_ref(self, t0: float) -> np.ndarray:
         out = np.zeros((self.N + 1, 6))
+        sample = getattr(self.traj_fn, "sample", None)
+        if sample is not None:  # same bits as the loop below (R_MJ_FROM_PIN is a signed permutation)
+            P, V, _ = sample(np.array([t0 + k * self.dt_ocp for k in range(self.N + 1)]))
+            out[:, :3] = P @ self.R_mj_from_pin - self.p_site_minus_frame_pin
+            out[:, 3:] = V @ self.R_mj_from_pin
+            return out
         for k in range(self.N + 1):
             p, v, _ = self.traj_fn(t0 + k * self.dt_ocp)
             out[k, :3] = self.R_mj_from_pin.T @ np.asarray(p, float) - self.p_site_minus_frame_pin
@@ -246,11 +252,7 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
                                      z_contact=z_contact, t_approach=0.55, ee_start=obs0.ee_pos.copy(), t_pre=0.25)
     t_cp = 0.8
 
-    def traj(tq):
-        p, vv, s = base(tq)
-        if s and float(tq) < t_cp + 0.2:
-            return np.asarray(base(t_cp)[0], float), np.zeros(3), True
-        return p, vv, s
+    traj = with_contact_hold(base, t_cp, 0.2)
 
     R_site_from_pin_ee, p_off = site_calibration(obs0)
     nominal.close()

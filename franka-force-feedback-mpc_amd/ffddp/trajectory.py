@@ -80,6 +80,65 @@ def make_approach_then_circle(
         v[1] = radius * omega * np.cos(th)
         return p, v, True
 
+    def sample(ts):
+        """traj at every time of ts at once: (P [n][3], V [n][3], surface [n]),
+        element for element the same arithmetic as traj (so the same bits)."""
+        t = np.asarray(ts, dtype=float).reshape(-1)
+        P, V = np.empty((t.size, 3)), np.empty((t.size, 3))
+        m_pre = (t < t_pre) if t_pre > 0.0 else np.zeros(t.size, bool)
+        m_app = ~m_pre & (t < t_pre + t_approach)
+        m_cir = ~(m_pre | m_app)
+
+        def blend_v(sel, p0, p1, tau, T):
+            s_lin = tau / T
+            sc = np.minimum(np.maximum(s_lin, 0.0), 1.0)
+            s_ = sc * sc * (3.0 - 2.0 * sc)
+            dsdt = 6.0 * sc * (1.0 - sc) / T
+            P[sel] = (1.0 - s_)[:, None] * p0 + s_[:, None] * p1
+            V[sel] = dsdt[:, None] * (p1 - p0)
+
+        if m_pre.any():
+            blend_v(m_pre, p_start, p_pre, t[m_pre], t_pre)
+        if m_app.any():
+            blend_v(m_app, p_pre if t_pre > 0.0 else p_start, p_contact_start, t[m_app] - t_pre, t_approach)
+        if m_cir.any():
+            th = omega * (t[m_cir] - (t_pre + t_approach))
+            P[m_cir, 0] = center[0] + radius * np.cos(th)
+            P[m_cir, 1] = center[1] + radius * np.sin(th)
+            P[m_cir, 2] = z_contact
+            V[m_cir, 0] = -radius * omega * np.sin(th)
+            V[m_cir, 1] = radius * omega * np.cos(th)
+            V[m_cir, 2] = 0.0
+        return P, V, m_cir.copy()
+
+    traj.sample = sample
+    return traj
+
+
+def with_contact_hold(base: Traj, t_contact_phase: float, t_hold: float = 0.2) -> Traj:
+    """The benchmark runner's wrapper (run_classical.py:246-264): for t_hold
+    after the contact onset the reference holds the onset point with zero
+    velocity.  Keeps base's vectorised sample()."""
+    t_cp, t_end = float(t_contact_phase), float(t_contact_phase) + float(t_hold)
+
+    def traj(t: float):
+        p, v, s = base(t)
+        if s and float(t) < t_end:
+            return np.asarray(base(t_cp)[0], float), np.zeros(3), True
+        return p, v, s
+
+    if hasattr(base, "sample"):
+        p_hold = np.asarray(base(t_cp)[0], float)
+
+        def sample(ts):
+            t = np.asarray(ts, dtype=float).reshape(-1)
+            P, V, S = base.sample(t)
+            h = S & (t < t_end)
+            P[h] = p_hold
+            V[h] = 0.0
+            return P, V, S
+
+        traj.sample = sample
     return traj
 
 
@@ -102,14 +161,6 @@ def benchmark_traj(ee_start_mj, radius: float = 0.10, omega: float = 1.5) -> Tup
         t_approach=t_approach, ee_start=np.asarray(ee_start_mj, float), t_pre=t_pre,
     )
     t_contact_phase = t_pre + t_approach
-    t_stab = 0.2
-
-    def traj(t: float):
-        p, v, s = base(t)
-        if s and float(t) < t_contact_phase + t_stab:
-            p_hold, _, _ = base(t_contact_phase)
-            return np.asarray(p_hold, float), np.zeros(3), True
-        return p, v, s
-
+    traj = with_contact_hold(base, t_contact_phase, 0.2)
     meta = dict(z_contact=z_contact, z_pre=z_pre, center=center, t_contact_phase=t_contact_phase)
     return traj, meta
