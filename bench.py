@@ -105,6 +105,24 @@ def pmc_traffic(variant, contact, B, N):
     return {k: v.get("hbm_bytes_per_solve") for k, v in tj.get("kernels", {}).items()}
 
 
+def sq_limiter(variant, contact, B, N):
+    """What the SQ counters of the same configuration show limits the kernels
+    (tools/pmc_sq2.sh -> tools/pmc_summary.py --json -> profiles/sq_latest.json),
+    if they are for this configuration: per kernel, the FMA share of VALU
+    instructions and the fractions of wave time VALU-active, LDS-active,
+    parked on s_waitcnt / barriers, and issue-stalled."""
+    f = ROOT / "profiles" / "sq_latest.json"
+    if not f.exists():
+        return None
+    try:
+        j = json.loads(f.read_text())
+    except ValueError:
+        return None
+    if j.get("config") != f"{variant}/{contact}/B{B}/N{N}":
+        return None
+    return {"source": j.get("source"), "summary": j.get("summary"), "kernels": j.get("kernels")}
+
+
 def cpu_baseline(cfg, batch, maxiter: int, budget_s: float) -> dict:
     """The C++ scalar BoxFDDP (oracle/cpu) on the host cores: OpenMP over the
     same instances, one per thread at a time; warm-up, then the median of 5
@@ -308,6 +326,10 @@ def main():
         "frac_survey_formula": tot_survey * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
         "frac_of_measured_copy": tot_bytes * args.steps / elapsed / 1e9 / HBM_MEASURED_GBS,
         "dominant_kernel": dominant,
+        # the bound named above is the metric's roofline; the
+        # kernels themselves are limited by their dependent chains (the SQ
+        # counters of this configuration, when profiles/ holds them)
+        "limiter": sq_limiter(args.variant, args.contact, B, N) if world == 1 else None,
     }
     if dominant is not None and traffic and traffic.get(dominant["name"]) is not None:
         dominant["traffic_per_launch"] = traffic[dominant["name"]] / dominant["launches_per_solve"]
@@ -366,10 +388,12 @@ def main():
         assert np.array_equal(pinned.xs, solver.xs) and np.array_equal(pinned.K, solver.K)
         pinned.close()
         del pin_in
-        # headline: page-locked inputs and outputs (a serving loop refills the
-        # same page-locked arrays every tick); pageable: fresh numpy arrays,
-        # staged and page-faulted in by the copies
-        host_io["value"] = host_io["pinned"]["value"]
+        # value: pageable numpy arrays in and out (fresh arrays, staged and
+        # page-faulted in by the copies; the definition of rounds 1-2);
+        # value_pinned: page-locked inputs and outputs (a serving loop
+        # refilling the same page-locked arrays every tick)
+        host_io["value"] = host_io["pageable"]["value"]
+        host_io["value_pinned"] = host_io["pinned"]["value"]
 
     if rank == 0:
         base = None

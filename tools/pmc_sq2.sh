@@ -12,5 +12,5 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" "SQ_INSTS_VALU S
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o r -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-profile --no-host-io --no-extras $BENCH_ARGS > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
 done
-python3 $R/tools/pmc_summary.py $O > $O/summary.txt
+python3 $R/tools/pmc_summary.py $O --json=$O/sq.json --config="${SQ_CONFIG:-classical/normal_1d/B4096/N30}" --source="tools/pmc_sq2.sh $BENCH_ARGS" > $O/summary.txt
 cat $O/summary.txt | head -60

@@ -24,8 +24,10 @@ def kclass(n):
     return m.group(0)[2:].replace(" ", "") if m else None
 
 
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+opts = dict(a[2:].split("=", 1) for a in sys.argv[1:] if a.startswith("--") and "=" in a)
 tot = defaultdict(lambda: defaultdict(float))
-for f in Path(sys.argv[1]).rglob("*counter_collection.csv"):
+for f in Path(args[0]).rglob("*counter_collection.csv"):
     for row in csv.DictReader(f.open()):
         low = {k.lower(): v for k, v in row.items()}
         c = kclass(low.get("kernel_name", ""))
@@ -52,3 +54,23 @@ for c, d in sorted(tot.items()):
     print(f"== {c}: waves {w:.0f}")
     for k in sorted(d):
         print(f"   {k:24s} total {d[k]:.4g}  per-wave {d[k]/w:.4g}")
+
+if "json" in opts:
+    # --json=OUT --config=classical/normal_1d/B4096/N30 --source=profiles/...: the
+    # ratios per kernel, for bench.py's roofline.limiter
+    import json
+
+    ks = {}
+    for c, d in sorted(tot.items()):
+        wc = d.get("SQ_WAVE_CYCLES", 0) or 1
+        ks[c] = {"waves": d.get("SQ_WAVES", 0),
+                 "fma_share_of_valu": d.get("SQ_INSTS_VALU_FMA_F64", 0.0) / (d.get("SQ_INSTS_VALU", 0.0) or 1),
+                 "valu_active": d.get("SQ_ACTIVE_INST_VALU", 0.0) / wc,
+                 "lds_active": d.get("SQ_ACTIVE_INST_LDS", 0.0) / wc,
+                 "waiting": d.get("SQ_WAIT_ANY", 0.0) / wc, "issue_stalled": d.get("SQ_WAIT_INST_ANY", 0.0) / wc,
+                 "lds_bank_conflicts_per_wave": d.get("SQ_LDS_BANK_CONFLICT", 0.0) / (d.get("SQ_WAVES", 0) or 1)}
+    big = sorted(ks, key=lambda c: -tot[c].get("SQ_WAVE_CYCLES", 0.0))[:4]
+    summ = opts.get("summary", "share of wave time VALU-active / waiting, by total wave time: " + "; ".join(
+        f"{c} {ks[c]['valu_active']:.0%} / {ks[c]['waiting']:.0%}" for c in big))
+    Path(opts["json"]).write_text(json.dumps({"config": opts.get("config"), "source": opts.get("source"),
+                                              "summary": summ, "kernels": ks}, indent=1) + "\n")
