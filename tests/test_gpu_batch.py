@@ -40,7 +40,7 @@ def _sub(batch, idx):
 # extended-precision solve of the same 8 instances the numpy oracle itself
 # is 1.7e-7 off in us, 1.4e-8 in K (9.9e-7 element-wise), the C++ baseline
 # 2.2e-7 / 3.7e-8 / 3.1e-6 (tools/ext_budget.py, profiles/r04_ext_budget.jsonl)
-SPREAD_TOL = {"tracking": (1e-10, 3e-10, 1e-5), "random": (2e-7, 2e-7, 1e-5)}
+SPREAD_TOL = {"tracking": (1e-10, 3e-10, 5e-8), "random": (2e-7, 2e-7, 3e-5)}  # K_elem observed 3.7e-9 / 2.7e-6
 
 
 @pytest.mark.parametrize("variant,B,regime", [("classical", 4096, "tracking"), ("classical", 517, "tracking"),

@@ -27,7 +27,7 @@ from ffddp import controller as CT  # noqa: E402
 from ffddp import fleet as FL  # noqa: E402
 from ffddp import plant as PL  # noqa: E402
 
-from helpers import check_outcome, closed_loop_pins, log_parity, make_batch, product_cfg, rel_err  # noqa: E402
+from helpers import check_outcome, closed_loop_pins, elem_err, log_parity, make_batch, product_cfg, rel_err  # noqa: E402
 from oracle_pool import solve_many  # noqa: E402
 
 
@@ -132,14 +132,16 @@ def test_c5_per_gpu_shape_point3d_n100(monkeypatch):
     # the solve-form oracle (K by Cholesky solves, the kernel's order): the
     # budget's N = 100 figure is ~1e-10 (tests/test_gpu_parity.py CASE_TOL)
     ref = solve_many(cfg, batch, sel, consts=fddp.Consts(gains_form="solve"))
-    e = dict(xs=0.0, us=0.0, K=0.0, cost=0.0)
+    e = dict(xs=0.0, us=0.0, K=0.0, cost=0.0, K_elem=0.0)
     for i, r in zip(sel, ref):
         assert bool(big.ok[i]) == r["ok"] and int(big.iter[i]) == r["iter"]
         assert int(big.stats[i, 1]) == r["trials"]
         for k in ("xs", "us", "K"):
             e[k] = max(e[k], rel_err(getattr(big, k)[i], r[k]))
         e["cost"] = max(e["cost"], rel_err(big.cost[i], r["cost"]))
+        e["K_elem"] = max(e["K_elem"], elem_err(big.K[i], r["K"]))
     log_parity(f"batch/point3d/N{N}/B{B}/solve_form", n=len(sel), **e)
-    assert max(e["xs"], e["us"], e["cost"]) < 1e-9 and e["K"] < 1e-9, e
+    # element-wise K: as tests/test_gpu_parity.py TOL_K_ELEM (N = 100 solve form observed 6.2e-9 there)
+    assert max(e["xs"], e["us"], e["cost"]) < 1e-9 and e["K"] < 1e-9 and e["K_elem"] < 2e-7, e
     big.close()
     small.close()

@@ -61,8 +61,20 @@ CROCODDYL_FORM_TOL = {
 }
 SOLVE_FORM = fddp.Consts(gains_form="solve")
 # element-wise K check |a - b| <= tol (1 + |b|) beside the block-scaled rel_err
-# (K mixes entries of 1e-3 .. 1e3, so rel_err alone lets the small ones drift)
-TOL_K_ELEM = 1e-5
+# (K mixes entries of 1e-3 .. 1e3, so rel_err alone lets the small ones drift):
+# ~10x the observed maxima (profiles/r04_parity_errors.jsonl: <= 1.6e-8 on the
+# well-conditioned cases, whose absolute errors are uniform over K, so the
+# element-wise figure of an entry near 0 is ~max|K| x the block figure)
+TOL_K_ELEM = 2e-7
+# case -> element-wise K tolerance where the block tolerance is above TOL_K
+CASE_TOL_K_ELEM = {
+    ("classical", "point3d", 1, 1): 5e-7,  # observed 4.4e-8
+}
+CROCODDYL_FORM_TOL_K_ELEM = {
+    ("classical", "point3d", 1, 0): 5e-6,  # observed 4.6e-7
+    ("classical", "point3d", 1, 1): 3e-5,  # observed 2.9e-6 (the explicit inverse's own error)
+    ("ff", "point3d", 1, 1): 2e-6,  # observed 2.0e-7
+}
 
 CASES = [
     ("classical", "normal_1d", 1, 0),
@@ -112,7 +124,7 @@ def test_calc_diff_matches_oracle(variant, contact, surf, cone):
         assert e < TOL_NODE, (k, e)
 
 
-def _check_solves(name, cfg, b, solver, ref, tol=TOL_SOLVE, tol_k=TOL_K):
+def _check_solves(name, cfg, b, solver, ref, tol=TOL_SOLVE, tol_k=TOL_K, tol_ke=TOL_K_ELEM):
     """Identical discrete path and close continuous outputs; logs the errors."""
     e = dict(xs=0.0, us=0.0, K=0.0, cost=0.0, K_elem=0.0)
     for i, r in enumerate(ref):
@@ -130,7 +142,7 @@ def _check_solves(name, cfg, b, solver, ref, tol=TOL_SOLVE, tol_k=TOL_K):
     totals = {k: int(sum(r[k] for r in ref)) for k in ("reg_retries", "forward_errors", "neg_branch", "clamped")}
     log_parity(name, B=len(ref), **e, **totals)
     assert e["xs"] < tol and e["us"] < tol and e["cost"] < tol, e
-    assert e["K"] < tol_k and e["K_elem"] < TOL_K_ELEM, e
+    assert e["K"] < tol_k and e["K_elem"] < tol_ke, e
     return totals
 
 
@@ -147,13 +159,14 @@ def test_solve_matches_oracle(variant, contact, surf, cone):
     if key in CROCODDYL_FORM_TOL:
         ref = solve_many(cfg, b, range(B), consts=SOLVE_FORM)
         tol, tol_k = CASE_TOL.get(key, (TOL_SOLVE, TOL_K))
-        _check_solves(name + "/solve_form", cfg, b, solver, ref, tol, tol_k)
+        _check_solves(name + "/solve_form", cfg, b, solver, ref, tol, tol_k, CASE_TOL_K_ELEM.get(key, TOL_K_ELEM))
         tol, tol_k = CROCODDYL_FORM_TOL[key]
+        tol_ke = CROCODDYL_FORM_TOL_K_ELEM.get(key, TOL_K_ELEM)
         name += "/crocoddyl_form"
     else:
-        tol, tol_k = TOL_SOLVE, TOL_K
+        tol, tol_k, tol_ke = TOL_SOLVE, TOL_K, TOL_K_ELEM
     ref = solve_many(cfg, b, range(B))
-    _check_solves(name, cfg, b, solver, ref, tol, tol_k)
+    _check_solves(name, cfg, b, solver, ref, tol, tol_k, tol_ke)
 
 
 def test_solve_random_regime_horizon30():
@@ -169,7 +182,7 @@ def test_solve_random_regime_horizon30():
     # implementation (this library, the oracle in both gains forms, the C++
     # baseline) is 1e-9..8e-9 from the extended-precision answer on the first
     # 8 instances (profiles/r03_ext_budget.jsonl); observed here 1.7e-8
-    _check_solves("solve/random/N30/B32", cfg, b, solver, ref, tol=2e-7, tol_k=4e-8)
+    _check_solves("solve/random/N30/B32", cfg, b, solver, ref, tol=2e-7, tol_k=4e-8, tol_ke=3e-6)  # K_elem 3.3e-7
 
 
 def test_solve_plain_fddp():
@@ -348,7 +361,8 @@ def test_long_horizon_point3d_matches_oracle():
     _check_solves("solve/point3d/N100/solve_form", cfg, b, solver, ref, tol=TOL_SOLVE, tol_k=TOL_K)
     # explicit-inverse oracle: its own error is 2.3e-8 / 6.3e-8 / K 2.3e-7
     ref = solve_many(cfg, b, range(B))
-    _check_solves("solve/point3d/N100/crocoddyl_form", cfg, b, solver, ref, tol=6e-7, tol_k=2e-6)
+    _check_solves("solve/point3d/N100/crocoddyl_form", cfg, b, solver, ref, tol=6e-7, tol_k=2e-6,
+                  tol_ke=1e-4)  # K_elem 8.5e-6: the explicit inverse's own error
 
 
 def test_gravity_torque_dev_matches_oracle():
