@@ -3,7 +3,8 @@
 # own time limit, stopping at the first failure.
 #   budget  GPU leg of the extended-precision error budget (tools/ext_budget_gpu.py)
 #   c1      configs[0] tick breakdown: solve plan, host-array solve, per-kernel events
-#   sq      SQ counters per kernel at B=4096 (tools/pmc_sq2.sh)
+#   sq      SQ counters per kernel at B=4096 and B=512 (tools/pmc_sq2.sh)
+#   gaps    kernel timelines of one solve at B=1 / 256 / 512 (time between kernels per queue)
 #   tests   pytest -m gpu with the parity log
 #   bench   one default bench line
 # usage: [STEPS="c1 tests"] tools/gpu_r04.sh TAG
@@ -20,7 +21,9 @@ for st in $STEPS; do
         timeout -k 10 120 python3 tools/c1_breakdown.py --time 4 --no-plan > $O/c1_noplan.log 2>&1
         timeout -k 10 120 python3 tools/c1_breakdown.py --time 4 --profile > $O/c1_prof.log 2>&1
         tail -qn1 $O/c1_plan.log $O/c1_noplan.log $O/c1_prof.log ;;
-    sq) BENCH_ARGS="--batch 4096" $R/tools/pmc_sq2.sh $TAG/sq4096 > $O/sq.log 2>&1 ;;
+    sq) BENCH_ARGS="--batch 4096" $R/tools/pmc_sq2.sh $TAG/sq4096 > $O/sq.log 2>&1
+        BENCH_ARGS="--batch 512" SQ_CONFIG=classical/normal_1d/B512/N30 $R/tools/pmc_sq2.sh $TAG/sq512 > $O/sq512.log 2>&1 ;;
+    gaps) for b in 1 256 512; do $R/tools/diag_timeline_b.sh $TAG/tl$b $b; grep "queue span" $O/tl$b/timeline.txt; done ;;
     tests) rm -f $O/parity.jsonl
         FFDDP_PARITY_LOG=$O/parity.jsonl timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
           --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }

@@ -2,8 +2,9 @@
 
 usage: python tools/timeline.py <dir with *kernel_trace.csv> [solve_index]
 Prints, for the chosen solve (default: the last one), every dispatch of the
-solver kernels as (stream/queue, kernel, start offset us, duration us), then a
-per-iteration sum per kernel class.
+solver kernels as (stream/queue, kernel, start offset us, duration us), then
+per queue the sum per kernel class and the time between consecutive kernels
+(what a single-launch solve could remove at most).
 """
 import csv
 import glob
@@ -45,3 +46,7 @@ for q, lst in per_q.items():
         print(f"   {k:14s} start {(a - t0) / 1e3:9.1f}  dur {(b - a) / 1e3:8.1f}")
         acc[k] += (b - a) / 1e3
     print("   totals: " + " ".join(f"{k}={v:.0f}" for k, v in acc.items()))
+    span = (lst[-1][1] - lst[0][0]) / 1e3
+    busy = sum(b - a for a, b, _ in lst) / 1e3
+    print(f"   queue span {span:.1f} us, kernels {busy:.1f} us ({busy / max(span, 1e-9):.1%}), gaps {span - busy:.1f} us "
+          f"over {len(lst) - 1} launch boundaries ({(span - busy) / max(len(lst) - 1, 1):.2f} us each)")
