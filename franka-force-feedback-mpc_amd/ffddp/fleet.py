@@ -31,11 +31,11 @@ from . import _abi
 from . import robot as R
 from .config import OcpConfig
 from .controller import _OCP_FIELDS, _quat_wxyz_to_R, classical_benchmark_config
-from .plant import BatchedPlant, PandaTablePlant, observation_from_record
+from .plant import BatchedPlant, PandaTablePlant
 from .runlog import summary_metrics
 from .solver import BatchedBoxFDDP
 from .trajectory import TABLE_CENTER, TABLE_HALF_Z, TOOL_RADIUS, make_approach_then_circle, with_contact_hold
-from .uncertainty import ScenarioUncertaintyInjector, config_for_scenario
+from .uncertainty import BatchedUncertaintyInjector, config_for_scenario
 
 Traj = Callable[[float], Tuple[np.ndarray, np.ndarray, bool]]
 
@@ -268,11 +268,11 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
                             p_site_minus_frame_pin=p_off, device=device)
     plant.set_tilt(tilt)  # hidden from the controllers
     plant.step(tau0 * 0.0, integrate=False)
-    inj = {}
-    for b in range(B):
-        uc = config_for_scenario(str(names[b]), seed=int(seed[b]))
-        if uc is not None:
-            inj[b] = ScenarioUncertaintyInjector(dt=plant.dt, nu=7, config=uc)
+    # the scenarios' uncertainty injectors, batched (BatchedUncertaintyInjector:
+    # draw for draw the per-instance ScenarioUncertaintyInjector)
+    ucfg = {b: config_for_scenario(str(names[b]), seed=int(seed[b])) for b in range(B)}
+    inj_idx = np.array([b for b in range(B) if ucfg[b] is not None], dtype=np.int64)
+    inj = BatchedUncertaintyInjector(dt=plant.dt, nu=7, configs=[ucfg[b] for b in inj_idx]) if inj_idx.size else None
     steps = int(total_time / plant.dt)
     series = {k: np.zeros((steps, B)) for k in ("t", "err_tan", "err_3d", "fn_meas", "contact")}
     # solver health per instance: ticks on the instability fallback
@@ -293,11 +293,9 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
     for k in range(steps):
         q, v, bias = obs[:, 0:7], obs[:, 7:14], obs[:, 14:21]
         fn, ee = obs[:, 46] * (obs[:, 47] > 0.5), obs[:, 28:31]
-        if inj:
+        if inj is not None:
             q, v = q.copy(), v.copy()
-            for b, j in inj.items():
-                d = j.observation_for_controller(observation_from_record(obs[b]))
-                q[b], v[b] = d.q, d.dq
+            q[inj_idx], v[inj_idx] = inj.observation_for_controller(q[inj_idx], v[inj_idx])
         tc = time.perf_counter()
         tau = mpc.compute_control(q, v, bias, fn, ee[:, 2], t)
         ctrl_s += time.perf_counter() - tc
@@ -310,8 +308,8 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
             rec_obs[k][:, 0:7], rec_obs[k][:, 7:14] = q[rec_idx], v[rec_idx]
             rec_tau[k] = tau[rec_idx]
         tau_app = tau * scale
-        for b, j in inj.items():
-            tau_app[b] = j.command_for_plant(tau[b])
+        if inj is not None:
+            tau_app[inj_idx] = inj.command_for_plant(tau[inj_idx])
         obs = plant.step(tau_app).copy()
         t += plant.dt
         p_ref, _, _ = traj(t)

@@ -108,3 +108,78 @@ class ScenarioUncertaintyInjector:
     def command_for_plant(self, tau_cmd_nominal) -> np.ndarray:
         self._cmd_hist.append(np.asarray(tau_cmd_nominal, dtype=float).reshape(self.nu).copy())
         return self._tau_hat()
+
+
+class BatchedUncertaintyInjector:
+    """ScenarioUncertaintyInjector for many instances at once (the closed-loop
+    fleet's actuation_uncertainty scenario): each instance keeps its own
+    seeded Generator and draws, in the scalar injector's order, the same
+    numbers -- per tick 7 + 7 + 7 normals for the observation (q, dq, torque
+    measurement) and 7 for the command -- pre-drawn a chunk of ticks at a time
+    (a Generator's normals are one stream however many a call asks for), and
+    the delay lines are ring buffers over the batch.  Only the fields the
+    fleet reads are produced: the delayed noisy (q, dq) and the applied
+    command.  Bit-identical to per-instance ScenarioUncertaintyInjector calls
+    (tests/test_closed_loop.py)."""
+
+    CHUNK = 256  # ticks of normals drawn per Generator call
+
+    def __init__(self, dt: float, nu: int, configs, tau_lpf_alpha: float = 0.2):
+        self.nu = int(nu)
+        self.dt = float(max(dt, 1.0e-9))
+        self.cfgs = list(configs)
+        self.B = len(self.cfgs)
+        c0 = self.cfgs[0] if self.cfgs else UncertaintyProfileConfig()
+        for c in self.cfgs:  # one delay / noise model (they differ by seed only)
+            if dataclasses.replace(c, seed=0) != dataclasses.replace(c0, seed=0):
+                raise ValueError("BatchedUncertaintyInjector: configs may differ by seed only")
+        self.rngs = [np.random.default_rng(int(c.seed)) for c in self.cfgs]
+        ab = [(float(r.uniform(float(c.a_min), float(c.a_max))), float(r.uniform(float(c.b_min), float(c.b_max))))
+              for r, c in zip(self.rngs, self.cfgs)]
+        self.a = np.array([x[0] for x in ab])
+        self.b = np.array([x[1] for x in ab])
+        self.obs_delay_steps = int(max(np.round(int(max(c0.delta_obs_cycles, 0)) * 1.0e-3 / self.dt), 0))
+        self.cmd_delay_steps = int(max(np.round(float(c0.delta_cmd_s) / self.dt), 0))
+        self.sig = (float(c0.sigma_q), float(c0.sigma_dq), float(c0.sigma_tau))
+        self._obs = None  # [D+1][B][14] ring of (q, dq); slot _oi is the oldest
+        self._oi = 0
+        self._cmd = np.zeros((self.cmd_delay_steps + 1, self.B, self.nu))
+        self._ci = 0
+        self._z = np.zeros((self.B, 0, 4 * self.nu))
+        self._zi = 0
+
+    def _normals(self):
+        """this tick's 28 normals per instance: q, dq, tau (observation), tau (command)"""
+        if self._zi >= self._z.shape[1]:
+            self._z = np.stack([r.standard_normal(self.CHUNK * 4 * self.nu).reshape(self.CHUNK, 4 * self.nu)
+                                for r in self.rngs])
+            self._zi = 0
+        z = self._z[:, self._zi]
+        self._zi += 1
+        return z
+
+    def _tau_hat(self, z7):
+        return self.a[:, None] * self._cmd[self._ci] + self.b[:, None] + (0.0 + self.sig[2] * z7)
+
+    def observation_for_controller(self, q, dq):
+        """(q, dq) [B][nu] -> the delayed, noisy (q, dq) the controllers see."""
+        nu = self.nu
+        cur = np.concatenate([np.asarray(q, float), np.asarray(dq, float)], 1)
+        if self._obs is None:
+            self._obs = np.repeat(cur[None], self.obs_delay_steps + 1, 0)
+            self._oi = 0
+        else:  # deque(maxlen).append: the oldest slot takes the newest entry
+            self._obs[self._oi] = cur
+            self._oi = (self._oi + 1) % (self.obs_delay_steps + 1)
+        old = self._obs[self._oi]
+        self._z_tick = z = self._normals()
+        qo = old[:, :nu] + (0.0 + self.sig[0] * z[:, :nu])
+        dqo = old[:, nu:] + (0.0 + self.sig[1] * z[:, nu:2 * nu])
+        self._tau_hat(z[:, 2 * nu:3 * nu])  # the torque measurement's draw (the fleet does not read it)
+        return qo, dqo
+
+    def command_for_plant(self, tau_cmd):
+        """tau_cmd [B][nu] -> the applied torques a * (delayed command) + b + noise."""
+        self._cmd[self._ci] = np.asarray(tau_cmd, float)
+        self._ci = (self._ci + 1) % (self.cmd_delay_steps + 1)
+        return self._tau_hat(self._z_tick[:, 3 * self.nu:])

@@ -119,3 +119,27 @@ def test_plant_press_settles_to_commanded_force():
     np.testing.assert_allclose(obs["f_world"], [0, 0, obs["fn"]], atol=1e-12)
     # the table holds the sphere near the surface (soft constraint: sub-mm penetration)
     assert abs(obs["ee_pos"][2] - (0.32 + 0.03)) < 2e-3
+
+
+@pytest.mark.parametrize("dt", [0.005, 0.001])
+def test_batched_injector_matches_scalar(dt):
+    """The fleet's BatchedUncertaintyInjector gives every instance exactly the
+    scalar injector's perturbed (q, dq) and applied command, tick for tick
+    (600 ticks: across the pre-draw chunk boundary; dt = 1 ms: delay lines)."""
+    seeds = [15, 1500003, 7, 42, 99]
+    cfgs = [U.config_for_scenario("actuation_uncertainty", seed=s) for s in seeds]
+    bat = U.BatchedUncertaintyInjector(dt=dt, nu=7, configs=cfgs)
+    sc = [U.ScenarioUncertaintyInjector(dt=dt, nu=7, config=c) for c in cfgs]
+    assert bat.obs_delay_steps == sc[0].obs_delay_steps and bat.cmd_delay_steps == sc[0].cmd_delay_steps
+    rng = np.random.default_rng(3)
+    for k in range(600):
+        q, dq, tau = rng.normal(size=(5, 7)), rng.normal(size=(5, 7)), rng.normal(size=(5, 7)) * 10
+        qb, dqb = bat.observation_for_controller(q, dq)
+        ab = bat.command_for_plant(tau)
+        for b, j in enumerate(sc):
+            o = _synthetic_obs(k, rng)
+            o.q, o.dq = q[b].copy(), dq[b].copy()
+            d = j.observation_for_controller(o)
+            np.testing.assert_array_equal(qb[b], d.q)
+            np.testing.assert_array_equal(dqb[b], d.dq)
+            np.testing.assert_array_equal(ab[b], j.command_for_plant(tau[b]))
