@@ -148,16 +148,23 @@ class FleetClassicalMPC:
             tref = _abi.gravity_torque(self.q_nom)
         else:
             tref = _abi.gravity_torque(q)
-        x0_d = torch.from_numpy(x0).to(self.dev)
+        # the tick's inputs go up as ONE copy (packed float64: x0, inst_ref,
+        # tau_prev, surface, warm-start mask per instance, then the shared
+        # node references), its outputs come down as one (below)
+        pk = np.concatenate([x0, xreg, tref, self.tau_prev, surface_now[:, None].astype(np.float64),
+                             self.valid[:, None].astype(np.float64)], 1)
+        up = torch.from_numpy(np.concatenate([pk.ravel(), self._node_ref(t).ravel()])).to(self.dev)
+        pk_d = up[: B * 44].view(B, 44)
+        x0_d = pk_d[:, 0:14]
         T["x0"].copy_(x0_d)
-        T["node_ref"].copy_(torch.from_numpy(self._node_ref(t)).to(self.dev).expand(B, N + 1, 6))
-        T["inst_ref"].copy_(torch.from_numpy(np.concatenate([xreg, tref], 1)).to(self.dev))
-        T["surface"].copy_(torch.from_numpy(surface_now.astype(np.uint8)).to(self.dev))
+        T["node_ref"].copy_(up[B * 44:].view(1, N + 1, 6).expand(B, N + 1, 6))
+        T["inst_ref"].copy_(pk_d[:, 14:35])
+        T["surface"].copy_(pk_d[:, 42].to(torch.uint8))
         # warm start (_shift_guess, :733-757): [x0] + xs[1:], us[1:] + [us[-1]]; cold: [x0]*(N+1), [tau_prev]*N
-        vmask = torch.from_numpy(self.valid).to(self.dev)
+        vmask = pk_d[:, 43] != 0
         xs_i = x0_d[:, None, :].expand(B, N + 1, 14).clone()
         xs_i[:, 1:] = torch.where(vmask[:, None, None], self.keep_xs[:, 1:], xs_i[:, 1:])
-        tp = torch.from_numpy(self.tau_prev).to(self.dev)[:, None, :].expand(B, N, 7)
+        tp = pk_d[:, 35:42][:, None, :].expand(B, N, 7)
         us_sh = torch.cat([self.keep_us[:, 1:], self.keep_us[:, -1:]], 1)
         T["xs_init"].copy_(xs_i)
         T["us_init"].copy_(torch.where(vmask[:, None, None], us_sh, tp))
@@ -168,16 +175,17 @@ class FleetClassicalMPC:
         self.keep_xs.copy_(torch.where(f3, T["xs"], self.keep_xs))
         self.keep_us.copy_(torch.where(f3, T["us"], self.keep_us))
         self.keep_K.copy_(torch.where(fin[:, None, None, None], T["K"], self.keep_K))
-        fin_h = fin.cpu().numpy()
-        self.valid |= fin_h
-        us0 = self.keep_us[:, 0].cpu().numpy()
-        xs0 = self.keep_xs[:, 0].cpu().numpy()
-        K0 = self.keep_K[:, 0].cpu().numpy()
-        cost = T["cost"].cpu().numpy()
-        iters = T["iters"].cpu().numpy()
-        ok = T["ok"].cpu().numpy().astype(bool)
-        neg_acc = T["stats"][:, 9].cpu().numpy()  # ascent-direction acceptances of this solve
-        fn_pred = np.where(surface_now, T["fn_pred"][:, 0].cpu().numpy(), np.nan)
+        f64 = torch.float64
+        down = torch.cat([fin.to(f64)[:, None], self.keep_us[:, 0], self.keep_xs[:, 0], self.keep_K[:, 0].reshape(B, 98),
+                          T["cost"][:, None], T["iters"].to(f64)[:, None], T["ok"].to(f64)[:, None],
+                          T["stats"][:, 9].to(f64)[:, None], T["fn_pred"][:, 0:1]], 1).cpu().numpy()
+        self.valid |= down[:, 0] != 0
+        us0, xs0, K0 = down[:, 1:8], down[:, 8:22], down[:, 22:120].reshape(B, 7, 14)
+        cost = down[:, 120].copy()
+        iters = down[:, 121].astype(np.int32)
+        ok = down[:, 122] != 0
+        neg_acc = down[:, 123].astype(np.int32)  # ascent-direction acceptances of this solve
+        fn_pred = np.where(surface_now, down[:, 124], np.nan)
         # _policy_control (:759-779): u = us[0] + s K[0] (x - xs[0])
         tau_raw = np.where(self.valid[:, None], us0, self.tau_prev)
         if cfg.use_feedback_policy:
