@@ -5,7 +5,7 @@ entry point: staging, copies, launches, wait), and the
 solve's kernels (per-class HIP-event sums, ffddp_profile_read).  Prints one
 JSON line.
 
-    python tools/c1_breakdown.py [--time 4] [--neg-step-rule 0] [--no-plan | --profile]
+    python tools/c1_breakdown.py [--time 4] [--neg-step-rule 0] [--no-plan | --profile] [--cpu]
 """
 from __future__ import annotations
 
@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--profile", action="store_true", help="per-kernel HIP events (adds event overhead; host-array"
                     " solve only: a plan captures no timing events)")
     ap.add_argument("--no-plan", action="store_true", help="plain host-array solve instead of the solve plan")
+    ap.add_argument("--cpu", action="store_true", help="also time the C++ scalar BoxFDDP (oracle/cpu, one thread) "
+                    "on every tick's problem, beside the GPU solve (the loop keeps the GPU results)")
     a = ap.parse_args()
     solve_s, iters, ctrl_s = [], [], []
     orig_solve = SV.BatchedBoxFDDP.solve
@@ -52,11 +54,27 @@ def main():
                 p[1] += n
         return r
 
+    cpu_s, cpu_same = [], []
+
     def run(self):
         t0 = time.perf_counter()
         r = orig_run(self)
         solve_s.append(time.perf_counter() - t0)
         iters.append(int(self.iter[0]))
+        if a.cpu:  # the same problem on one host core (checker leg: oracle/cpu)
+            import types
+
+            from ffddp import _abi
+            from oracle import cpu_fddp
+
+            b = types.SimpleNamespace(x0=self.x0, node_ref=self.node_ref, inst_ref=self.inst_ref,
+                                      surface=self.surface, xs_init=self.xs_init, us_init=self.us_init)
+            sp = self.solver.solver_params
+            t1 = time.perf_counter()
+            out = cpu_fddp.solve_batch(_abi.robot_struct(), self.solver._cfg_struct, b, self.maxiter, False, 1,
+                                       solver_params=sp)
+            cpu_s.append(time.perf_counter() - t1)
+            cpu_same.append(int(out["iter"][0]) == int(self.iter[0]) and bool(out["ok"][0]) == bool(self.ok[0]))
         return r
 
     def cc(self, obs, t):
@@ -80,6 +98,10 @@ def main():
            "controller_ms": 1e3 * float(np.mean(ctrl_s[sl])), "solve_call_ms": 1e3 * float(np.mean(solve_s[sl])),
            "solve_call_ms_p50": 1e3 * float(np.median(solve_s[sl])), "mean_iters": float(np.mean(iters[sl])),
            "host_controller_ms": 1e3 * float(np.mean(np.array(ctrl_s[sl]) - np.array(solve_s[sl])))}
+    if a.cpu:
+        out["cpu_solve_ms"] = 1e3 * float(np.mean(cpu_s[sl]))
+        out["cpu_solve_ms_p50"] = 1e3 * float(np.median(cpu_s[sl]))
+        out["cpu_same_iters_ok_frac"] = float(np.mean(cpu_same))
     if a.profile:
         out["kernels_ms_per_solve"] = {k: v[0] / n for k, v in prof.items() if v[1]}
         out["launches_per_solve"] = {k: v[1] / n for k, v in prof.items() if v[1]}

@@ -17,7 +17,7 @@ STEPS=${STEPS:-"budget c1 sq tests bench"}
 for st in $STEPS; do
   case $st in
     budget) timeout -k 10 120 python3 tools/ext_budget_gpu.py $O/ext_gpu.npz > $O/ext.log 2>&1 ;;
-    c1) timeout -k 10 120 python3 tools/c1_breakdown.py --time 4 > $O/c1_plan.log 2>&1
+    c1) timeout -k 10 200 python3 tools/c1_breakdown.py --time 4 --cpu > $O/c1_plan.log 2>&1
         timeout -k 10 120 python3 tools/c1_breakdown.py --time 4 --no-plan > $O/c1_noplan.log 2>&1
         timeout -k 10 120 python3 tools/c1_breakdown.py --time 4 --profile > $O/c1_prof.log 2>&1
         tail -qn1 $O/c1_plan.log $O/c1_noplan.log $O/c1_prof.log ;;
