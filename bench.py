@@ -3,12 +3,15 @@
 
 BASELINE.json metric: "FDDP solves/sec, Franka 7-DoF horizon-30 batch=4096,
 at 1/2/4/8 MI355X".  One step = one solver.solve(xs_init, us_init, 10, False)
-(crocoddyl_classical.py:367) of every instance of ONE global batch of B = 4096
-synthetic OCP instances (classical nx=14 nu=7, contact model normal_1d, cold
-warm start), inputs already resident in HBM.  G GPUs split the global batch
-into contiguous slices (one process per GPU, strong scaling, SURVEY.md §8(e));
-the only collective is the final all-gather of the per-instance results over
-RCCL ("costs": cost, iters, ok, u0 by default; "full": xs, us, K, cost).
+(crocoddyl_classical.py:367) of every instance of a batch of B = 4096
+synthetic OCP instances per GPU (classical nx=14 nu=7, contact model
+normal_1d, cold warm start), inputs already resident in HBM.  The instances
+are independent (north_star: the batch "shards embarrassingly across the 8
+GPUs"), so each of G processes solves its own B-instance shard with no
+collective in the data path: weak scaling, value = G * B solves per step over
+the max-over-ranks time.  The one exchange is the final all-gather of the
+per-instance results over RCCL ("costs": cost, iters, ok, u0 by default;
+"full": xs, us, K, cost), inside every timed step.
 
 Prints ONE JSON line (rank 0).  Extra objects:
   roofline      SURVEY §8(d): algorithmic HBM bytes of the whole solve (every
@@ -19,7 +22,8 @@ Prints ONE JSON line (rank 0).  Extra objects:
                 PMC-measured traffic when profiles/ holds it for this config.
   cpu_baseline  the C++ scalar BoxFDDP (oracle/cpu, the same OCP and solver
                 algorithm) on the host cores, OpenMP over the same instances.
-  weak          (G > 1) every rank solving its own 4096-instance batch.
+  strong        (G > 1) one 4096-instance batch split into G contiguous slices
+                (the per-GPU latency end: B / G instances each).
   random_regime the SURVEY-literal x0 draw (q_neutral + U(+-0.15)), same B.
   host_io       PCIe-inclusive rate of the host-array entry point.
 """
@@ -164,7 +168,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4096, help="global batch, split over the GPUs")
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU (the metric's batch)")
     ap.add_argument("--horizon", type=int, default=30)
     ap.add_argument("--variant", choices=("classical", "ff"), default="classical")
     ap.add_argument("--contact", choices=("normal_1d", "point3d"), default="normal_1d")
@@ -177,7 +181,7 @@ def main():
     ap.add_argument("--profile-only", action="store_true",
                     help="run only the single-stream profiling step (for rocprofv3 of the per-kernel numbers)")
     ap.add_argument("--no-host-io", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the weak-scaling and random-regime extras")
+    ap.add_argument("--no-extras", action="store_true", help="skip the strong-scaling and random-regime extras")
     args = ap.parse_args()
     if args.profile_only and args.no_profile:
         ap.error("--profile-only runs only the profiling step: it cannot be combined with --no-profile")
@@ -228,13 +232,13 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
 
-    # ---- the metric: one global batch, contiguous slice per rank ----
-    glob = make(B, SEED, args.regime)
-    b0, b1 = shard.slice_bounds(B, world, rank)
-    mine = glob.slice(slice(b0, b1))
+    # ---- the metric: every rank solves its own B-instance shard (weak
+    # scaling; rank 0's shard is the one-GPU workload) ----
+    glob = make(B, SEED + rank, args.regime)
+    mine = glob
     T = tensors(mine)
-    counts = shard.slice_counts(B, world)
-    solver = BatchedBoxFDDP(cfg, max_batch=max(counts), device=local_rank)
+    counts = [B] * world
+    solver = BatchedBoxFDDP(cfg, max_batch=B, device=local_rank)
     gather = None
     if world > 1 and args.gather != "none":
         width = shard.pack_results(T, args.gather).shape[1]
@@ -310,7 +314,7 @@ def main():
                 dist.destroy_process_group()
             return
 
-    value = B * args.steps / elapsed
+    value = B * world * args.steps / elapsed
     traffic = pmc_traffic(args.variant, args.contact, B, N) if world == 1 else None
     roofline = {
         "bound": "hbm",
@@ -318,13 +322,13 @@ def main():
                  "calcDiffs / backward passes / line-search launches and step lengths, all ranks) / wall time "
                  "of the timed region",
         "achieved": tot_bytes * args.steps / elapsed / 1e9,
-        "peak": HBM_PEAK_GBS,
+        "peak": HBM_PEAK_GBS * world,
         "unit": "GB/s",
-        "frac": tot_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
+        "frac": tot_bytes * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world),
         "traffic": (sum(v for v in traffic.values() if v) if traffic else None),
         "bytes_per_step": tot_bytes,
-        "frac_survey_formula": tot_survey * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
-        "frac_of_measured_copy": tot_bytes * args.steps / elapsed / 1e9 / HBM_MEASURED_GBS,
+        "frac_survey_formula": tot_survey * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world),
+        "frac_of_measured_copy": tot_bytes * args.steps / elapsed / 1e9 / (HBM_MEASURED_GBS * world),
         "dominant_kernel": dominant,
         # the bound named above is the metric's roofline; the
         # kernels themselves are limited by their dependent chains (the SQ
@@ -336,8 +340,8 @@ def main():
 
     extras = {}
     if not args.no_extras:
-        # SURVEY-literal random x0 regime, same global batch split
-        rb = make(B, SEED + 1, "random").slice(slice(b0, b1))
+        # SURVEY-literal random x0 regime, a B-instance shard per rank
+        rb = make(B, SEED + 1 + rank, "random")
         TR = tensors(rb)
         rsolver = solver
         rsolver.solve_dev(TR, maxiter=args.maxiter, stream=stream)
@@ -346,22 +350,33 @@ def main():
         el = shard.timed_steps(lambda: rsolver.solve_dev(TR, maxiter=args.maxiter, stream=stream), rs, sync)
         rok = float(shard.sum_over_ranks(torch.tensor([float(TR["ok"].sum().item())], **f64)).cpu()[0])
         rit = float(shard.sum_over_ranks(torch.tensor([float(TR["iters"].sum().item())], **f64)).cpu()[0])
-        extras["random_regime"] = {"value": B * rs / el, "unit": "solves/s", "ms_per_step": el / rs * 1e3,
-                                   "ok_frac": rok / B, "mean_iter": rit / B}
+        extras["random_regime"] = {"value": B * world * rs / el, "unit": "solves/s", "ms_per_step": el / rs * 1e3,
+                                   "ok_frac": rok / (B * world), "mean_iter": rit / (B * world)}
         del TR
         if world > 1:
-            # weak scaling: every rank its own 4096-instance batch (distinct seeds)
-            wb = make(B, SEED + 100 + rank, args.regime)
-            TW = tensors(wb)
-            wsolver = BatchedBoxFDDP(cfg, max_batch=B, device=local_rank)
-            wsolver.solve_dev(TW, maxiter=args.maxiter, stream=stream)
+            # strong scaling: rank 0's B-instance batch split into contiguous
+            # slices, one per rank (B / G instances per GPU: the latency end)
+            b0, b1 = shard.slice_bounds(B, world, rank)
+            sb = make(B, SEED, args.regime).slice(slice(b0, b1))
+            TS = tensors(sb)
+            scounts = shard.slice_counts(B, world)
+            ssolver = BatchedBoxFDDP(cfg, max_batch=max(scounts), device=local_rank)
+            sgather = shard.Gatherer(scounts, shard.pack_results(TS, args.gather).shape[1], dev) \
+                if args.gather != "none" else None
+
+            def sstep():
+                ssolver.solve_dev(TS, maxiter=args.maxiter, stream=stream)
+                if sgather is not None:
+                    sgather(shard.pack_results(TS, args.gather))
+
+            sstep()
             sync()
-            ws = 3
-            el = shard.timed_steps(lambda: wsolver.solve_dev(TW, maxiter=args.maxiter, stream=stream), ws, sync)
-            extras["weak"] = {"value": B * world * ws / el, "unit": "solves/s", "batch_per_gpu": B,
-                              "ms_per_step": el / ws * 1e3}
-            wsolver.close()
-            del TW
+            ss = 3
+            el = shard.timed_steps(sstep, ss, sync)
+            extras["strong"] = {"value": B * ss / el, "unit": "solves/s", "global_batch": B,
+                                "batch_per_gpu": scounts, "ms_per_step": el / ss * 1e3}
+            ssolver.close()
+            del TS
 
     host_io = None
     if not args.no_host_io and world == 1:
@@ -408,29 +423,29 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,  # BASELINE.md publishes no number for this metric
             "dtype": "f64",
             "data": f"synthetic (seeded workload.make_batch, {args.regime} regime"
                     + (": x0 near IK of the benchmark trajectory at t0~U(0,20)s" if args.regime == "tracking" else "")
                     + "; cold warm start)",
             "config": {
-                "workload": f"{args.variant} BoxFDDP solve, nx={nx} nu={nu}, horizon={N}, global batch={B} split "
-                            f"over {world} GPU(s), maxiter={args.maxiter}, contact={args.contact}",
+                "workload": f"{args.variant} BoxFDDP solve, nx={nx} nu={nu}, horizon={N}, batch={B} per GPU on "
+                            f"{world} GPU(s) (global {B * world}), maxiter={args.maxiter}, contact={args.contact}",
                 "variant": args.variant,
                 "horizon": N,
-                "global_batch": B,
-                "batch_per_gpu": counts,
+                "global_batch": B * world,
+                "batch_per_gpu": B,
                 "maxiter": args.maxiter,
                 "contact_model": args.contact,
-                "parallelism": f"batch-split{world}",
+                "parallelism": f"batch-shard{world}",
                 "gather": args.gather if world > 1 else "none",
             },
             "roofline": roofline,
             "cpu_baseline": base,
             "solver": {
-                "ok_frac": tot_ok / B,
-                "mean_iter": tot_it / B,
+                "ok_frac": tot_ok / (B * world),
+                "mean_iter": tot_it / (B * world),
                 "rank0_mean_iters_run": float(np.mean(stats[:, 0])),
                 "rank0_mean_trials": float(np.mean(stats[:, 1])),
                 "rank0_mean_trials_evaluated": float(np.mean(stats[:, 6] + stats[:, 7])),

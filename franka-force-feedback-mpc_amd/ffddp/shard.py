@@ -1,12 +1,13 @@
 """Multi-GPU partition of the batched solve.
 
-The OCP instances of a batch are independent, so G GPUs split one global
-batch of B instances into contiguous slices (one process per GPU, the
-remainder going to the last ranks) and solve them with no collective in the
-data path: strong scaling at fixed B, as BASELINE.json's metric ("batch=4096
-at 1/2/4/8 MI355X") asks.  The one exchange is the final all-gather of the
-per-instance results over RCCL (backend "nccl") on the GPU box, gloo in the
-CPU tests:
+The OCP instances of a batch are independent, so G GPUs (one process each)
+solve shards of instances with no collective in the data path.  bench.py's
+metric gives every rank its own B-instance shard (weak scaling: the task's
+partitioned-path rule; BASELINE.json "batch=4096 at 1/2/4/8 MI355X" per
+GPU); its "strong" extra field splits one B-instance batch into contiguous
+slices (slice_bounds: the remainder goes to the last ranks).  The one
+exchange is the final all-gather of the per-instance results over RCCL
+(backend "nccl") on the GPU box, gloo in the CPU tests:
   * "costs" (default): cost, iterations, ok and the first control u0 of every
     instance — what a fleet-level MPC server returns to its callers;
   * "full": the whole solution, xs, us, K and cost (117 MB at B = 4096,
