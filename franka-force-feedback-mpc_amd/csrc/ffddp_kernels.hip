@@ -1127,8 +1127,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 //               issues the prefetch of the one after,
 //   E, G        wave 0 (one column / state component per lane, as before).
 // ---------------------------------------------------------------------------
-template <bool FF>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void k_backward_w2(
+// WPE: waves per SIMD the register budget allows.  1 (296 registers) for
+// small slices, where the pass is the solve's chain; 2 (256, some spilled)
+// in the tails of large slices, where a block that needs two whole SIMDs
+// waits for the other slices' kernels to drain them: at 2 its waves share a
+// SIMD with one of theirs (B = 4096: +2 % over the one-wave LATE variant
+// there).  Same arithmetic either way.
+template <bool FF, int WPE = 1>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void k_backward_w2(
     const DevConsts* __restrict__ Cg, Dev d, int iter, int cur, int w2_max) {
   using S_t = BwW<FF>;
   constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
@@ -2428,19 +2434,32 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
         ProfScope p(h, ss, KC_BACKWARD);
         const int lmax = h->bw_late_max >= 0 ? h->bw_late_max : h->n_simd / S;
         // two-wave variant: for slices no larger than one wave per SIMD share
-        // (small per-GPU batches, where the whole solve is latency-bound); in
-        // the tail of large slices the other slices' kernels hold the SIMDs and
-        // its 2-wave blocks wait for them (B = 4096: -1.7 %)
-        const int w2auto = Bk <= h->n_simd / S ? h->n_simd / (2 * S) : 0;
+        // (small per-GPU batches, where the whole solve is latency-bound) at
+        // one wave per SIMD; in the tails of large slices (active count up to
+        // lmax) at two waves per SIMD, so its blocks need not wait for the
+        // other slices' kernels to free whole SIMDs (the one-wave kernel there:
+        // B = 4096 -1.7 %; this one +2 % over LATE).  FF's
+        // two-wave pass spills too much at two waves per SIMD: LATE there.
+        const bool small = Bk <= h->n_simd / S;
+        const int w2auto = small ? h->n_simd / (2 * S) : (FF ? 0 : lmax);
         const int w2max = std::min(lmax, h->bw_w2_max >= 0 ? h->bw_w2_max : w2auto);
         if (lmax < Bk)
           hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1, lmax, w2max);
         if (lmax > w2max && w2max < Bk)
           hipLaunchKernelGGL((k_backward_w<FF, true>), dim3(lmax < Bk ? lmax : Bk), dim3(64), 0, ss, h->dc, d, it, it & 1,
                              lmax, w2max);
-        if (w2max > 0)
-          hipLaunchKernelGGL((k_backward_w2<FF>), dim3(w2max < Bk ? w2max : Bk), dim3(128), 0, ss, h->dc, d, it, it & 1,
-                             w2max);
+        if (w2max > 0) {
+          const dim3 g2(w2max < Bk ? w2max : Bk);
+          if constexpr (!FF) {
+            if (!small) {
+              hipLaunchKernelGGL((k_backward_w2<FF, 2>), g2, dim3(128), 0, ss, h->dc, d, it, it & 1, w2max);
+            } else {
+              hipLaunchKernelGGL((k_backward_w2<FF, 1>), g2, dim3(128), 0, ss, h->dc, d, it, it & 1, w2max);
+            }
+          } else {
+            hipLaunchKernelGGL((k_backward_w2<FF, 1>), g2, dim3(128), 0, ss, h->dc, d, it, it & 1, w2max);
+          }
+        }
       }
       int n1 = NTRIALS;
       {
