@@ -34,6 +34,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "ffddp_consts.hpp"
@@ -528,6 +529,7 @@ template <bool FF> struct BwW {
   int spec;           // k_backward_w2: wave 1's K (and LLT k) from L1 are valid
   double Vx[NX], Qv[ND], kk[NU], z[NU];
   double fs[64], kp[64], uu[64], ulb[64], uub[64];  // one slot per lane: written without lane guards
+  double fsb[2][64];  // k_backward_w2: node t's gap in slot t & 1 (staged before node t+1's phase G reads its own)
   int flag;
   int badw[2];  // k_backward_w2: per-wave NaN flags of phases F / G
   int clamped[NU];
@@ -917,7 +919,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       // ---- phase C: Q lower triangle (mirrored), entries fixed per lane ----
 #pragma unroll QC_N
       for (int k = 0; k < NQL; ++k) {
-        if (l + 64 * k < NQE) {
+        // no range guard: a lane past the last entry holds entry (0, 0)
+        // (qrc's default) and writes the same bits as the lane that owns it,
+        // so the passes need no divergent branch and can interleave
+        {
           const int r = qrc[k] >> 8, c = qrc[k] & 255;
           double lv;
           if (r < NX)
@@ -1248,18 +1253,19 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       int badv = badf;
       if (l < NX) {
         double vfs = 0.0;
+        const double* fsg = S.fsb[tg & 1];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
+        for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * fsg[i];
         double vx = S.Qv[l];
 #pragma unroll
         for (int c = 0; c < NU; ++c) vx -= S.K[c * NX + l] * S.Qv[NX + c];
         if (!feas) vx += vfs;
         badv |= bad(fabs(vx)) ? 1 : 0;
-        ffl = fmax(ffl, fabs(S.fs[l]));
+        ffl = fmax(ffl, fabs(fsg[l]));
         if (!feas) {
           d.w[((long)b * (N + 1) + tg) * NX + l] = vfs;
-          cdg -= vx * S.fs[l];
-          cdq += S.fs[l] * vfs;
+          cdg -= vx * fsg[l];
+          cdq += fsg[l] * vfs;
         }
         if (l < NU) {
           double quk = 0.0;
@@ -1285,19 +1291,24 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // barrier less per node), then this node's gap / warm start / control
       // (record t is in LDS) ----
       if (wv == 0) {
-        if (t < N - 1) {
-          phase_g(t + 1);
-          // z below reads Vx entries other lanes of this wave just wrote
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-        }
-        S.fs[l] = pfs;
+        // staging first: its wait for the loads prefetched one node ago
+        // would otherwise also wait for phase G's global stores (w, k) just
+        // issued (vmcnt counts loads and stores in issue order, and the
+        // lane-guarded stores leave the compiler only vmcnt(0)); staged
+        // here, the stores have a whole node to complete before the next wait
+        S.fsb[t & 1][l] = pfs;
         S.kp[l] = pkp;
         S.uu[l] = pus;
         const int tn = t > 0 ? t - 1 : 0;
         pfs = d.fs[((long)b * (N + 1) + tn) * NX + lx];
         pkp = d.k[((long)b * N + tn) * NU + lu];
         pus = d.us[((long)b * N + tn) * NU + lu];
+        if (t < N - 1) {
+          phase_g(t + 1);
+          // z below reads Vx entries other lanes of this wave just wrote
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        }
       }
       PP(0);
       const double* Ar = S.R + rec_off_A();
@@ -1332,15 +1343,27 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         double Acol[NU];
 #pragma unroll
         for (int n = 0; n < NU; ++n) Acol[n] = ac * Ar[cc * 7 + n];
-        const int m0 = wv == 0 ? 0 : 4, m1 = wv == 0 ? 4 : NU;
+        // columns [M0, M1) with compile-time bounds, so their independent
+        // 7-term chains interleave (a runtime column range kept each column in
+        // a basic block of its own: one LDS round trip and one dependent
+        // chain after another)
+        auto mcols = [&](auto m0c, auto m1c) {
+          constexpr int M0 = decltype(m0c)::value, M1 = decltype(m1c)::value;
+          double h[M1 - M0];
 #pragma unroll
-        for (int m = 0; m < NU; ++m) {
-          if (m < m0 || m >= m1) continue;
-          double h = 0.0;
+          for (int m = M0; m < M1; ++m) {
+            h[m - M0] = 0.0;
 #pragma unroll
-          for (int n = 0; n < NU; ++n) h += Acol[n] * S.Y[n * NU + m];
-          S.M[c * NU + m] = (a0 * S.W[r0 * NU + m] + a1 * S.W[r1 * NU + m]) + 0.5 * h;
-        }
+            for (int n = 0; n < NU; ++n) h[m - M0] += Acol[n] * S.Y[n * NU + m];
+          }
+#pragma unroll
+          for (int m = M0; m < M1; ++m)
+            S.M[c * NU + m] = (a0 * S.W[r0 * NU + m] + a1 * S.W[r1 * NU + m]) + 0.5 * h[m - M0];
+        };
+        if (wv == 0)
+          mcols(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+        else
+          mcols(std::integral_constant<int, 4>{}, std::integral_constant<int, NU>{});
         if (wv == 1) {
           double qv = (c < NX) ? S.R[rec_off_Lx(NX) + c] : S.R[rec_off_Lu(NX) + c - NX];
           qv += a0 * S.Vx[r0] + a1 * S.Vx[r1];
@@ -1354,7 +1377,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // ---- phase C: Q lower triangle (mirrored), entries over 128 lanes ----
 #pragma unroll
       for (int k = 0; k < NQL; ++k) {
-        if (tid + 128 * k < NQE) {
+        // no range guard: a lane past the last entry holds entry (0, 0)
+        // (qrc's default) and writes the same bits as the lane that owns it,
+        // so the passes need no divergent branch and can interleave
+        {
           const int r = qrc[k] >> 8, c = qrc[k] & 255;
           double lv;
           if (r < NX)
