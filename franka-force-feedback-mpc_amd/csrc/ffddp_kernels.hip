@@ -1156,6 +1156,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (st->done) return;
 #ifdef FFDDP_PHASE_PROF
   const bool pp_on = (b == 0) && tid == 0;
+  unsigned long long dwave = 0;
 #endif
   PP_INIT();
   __shared__ S_t S;
@@ -1415,6 +1416,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       lds_sync();
       PP(3);
+#ifdef FFDDP_PHASE_PROF
+      const unsigned long long dwt0 = __builtin_readcyclecounter();
+#endif
       // ---- phase D: gains on wave 0 (rows on lanes 0..6); wave 1 stages the
       // next node's record (S.R is not read after phase C) ----
       if (wv == 0) {
@@ -1502,6 +1506,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         if (l == 0) S.spec = ok1 ? 1 : 0;
       }
+#ifdef FFDDP_PHASE_PROF
+      // development: each wave's own phase-D time (instance 0) into g_pp[28 + wave]
+      if (b == 0 && l == 0) dwave += __builtin_readcyclecounter() - dwt0;
+#endif
       lds_sync();
       PP(4);
       if (S.flag == 0) {
@@ -1590,6 +1598,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
     lds_sync();
   }
   PP_FLUSH();
+#ifdef FFDDP_PHASE_PROF
+  if (b == 0 && l == 0) atomicAdd(&g_pp[28 + wv], dwave);
+#endif
   if (tid == 0) {
     st->preg = preg;
     st->n_retries += retries;
