@@ -22,10 +22,21 @@ Prints ONE JSON line (rank 0).  Extra objects:
                 PMC-measured traffic when profiles/ holds it for this config.
   cpu_baseline  the C++ scalar BoxFDDP (oracle/cpu, the same OCP and solver
                 algorithm) on the host cores, OpenMP over the same instances.
-  strong        (G > 1) one 4096-instance batch split into G contiguous slices
-                (the per-GPU latency end: B / G instances each).
-  random_regime the SURVEY-literal x0 draw (q_neutral + U(+-0.15)), same B.
+  strong        (G > 1) the other reading of the metric, with the same fields
+                as the headline (value, ms_per_step, scaling "strong",
+                roofline): one 4096-instance batch split into G contiguous
+                slices (B / G instances per GPU: the per-GPU latency end).
+  random_regime the SURVEY-literal x0 draw (q_neutral + U(+-0.15)), same B,
+                with its own roofline.
+  ff            the force-feedback variant (nx = 21) at the metric's batch
+                and horizon, with its own roofline.
   host_io       PCIe-inclusive rate of the host-array entry point.
+roofline.fp64 prices the same run against the measured fp64 VALU peak
+(tools/micro/fp64_peak.hip -> profiles/r05_fp64_peak.json): issued fp64
+lane-flops per node stage / backward node / trial node from a PMC pass of
+this configuration (tools/pmc_fp64.sh -> profiles/fp64_latest.json) x the
+device-counted units of this run.  roofline.bound names the roof the run is
+closer to; roofline.frac stays SURVEY §8(d)'s HBM fraction.
 """
 from __future__ import annotations
 
@@ -127,6 +138,70 @@ def sq_limiter(variant, contact, B, N):
     return {"source": j.get("source"), "summary": j.get("summary"), "kernels": j.get("kernels")}
 
 
+def _profile_json(name, variant, contact, B, N):
+    f = ROOT / "profiles" / name
+    if not f.exists():
+        return None
+    try:
+        j = json.loads(f.read_text())
+    except ValueError:
+        return None
+    return j if j.get("config") == f"{variant}/{contact}/B{B}/N{N}" else None
+
+
+def fp64_peak_tflops():
+    """Measured fp64 FMA throughput of one MI355X (tools/micro/fp64_peak.hip)."""
+    f = ROOT / "profiles" / "r05_fp64_peak.json"
+    try:
+        return float(json.loads(f.read_text())["peak_fp64_fma_tflops"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def solve_units(stats: np.ndarray, N: int) -> dict:
+    """Device-counted work units of one batched solve: node stages (calcDiffs
+    x (N + 1)), backward nodes (backward passes x N), line-search trial nodes
+    (evaluated step lengths x (N + 1))."""
+    s = stats.astype(np.float64)
+    return {"node": float(s[:, 4].sum()) * (N + 1), "backward": float(s[:, 0].sum()) * N,
+            "forward": float((s[:, 6] + s[:, 7]).sum()) * (N + 1)}
+
+
+def solve_counts(stats: np.ndarray) -> dict:
+    s = stats.astype(np.float64)
+    return {"calcdiff": float(s[:, 4].sum()), "backward": float(s[:, 0].sum()),
+            "trials": float((s[:, 6] + s[:, 7]).sum()), "forward_launches": float(s[:, 5].sum())}
+
+
+def fp64_flops(stats, N, per_unit) -> float | None:
+    """Issued fp64 lane-flops of one batched solve: the PMC per-unit figures
+    (tools/pmc_fp64.py) x this solve's device-counted units."""
+    if not per_unit:
+        return None
+    u = solve_units(stats, N)
+    k = per_unit.get("kernels", {})
+    tot = 0.0
+    for c in ("node", "backward", "forward"):
+        if c not in k or "lane_flops_per_unit" not in k[c]:
+            return None
+        tot += k[c]["lane_flops_per_unit"] * u[c]
+    # the per-solve kernels (init, accept, commit, finalize): as profiled
+    tot += sum(v.get("lane_flops_per_solve", 0.0) for c, v in k.items() if c not in ("node", "backward", "forward"))
+    return tot
+
+
+def rooflines(bytes_per_step, flops_per_step, sec_per_step, world):
+    """HBM and fp64-VALU fractions of one timed configuration (all ranks)."""
+    hbm = {"achieved": bytes_per_step / sec_per_step / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s"}
+    hbm["frac"] = hbm["achieved"] / hbm["peak"]
+    pk = fp64_peak_tflops()
+    fp = None
+    if flops_per_step is not None and pk:
+        fp = {"achieved": flops_per_step / sec_per_step / 1e12, "peak": pk * world, "unit": "TFLOP/s"}
+        fp["frac"] = fp["achieved"] / fp["peak"]
+    return hbm, fp
+
+
 def cpu_baseline(cfg, batch, maxiter: int, budget_s: float) -> dict:
     """The C++ scalar BoxFDDP (oracle/cpu) on the host cores: OpenMP over the
     same instances, one per thread at a time; warm-up, then the median of 5
@@ -181,7 +256,11 @@ def main():
     ap.add_argument("--profile-only", action="store_true",
                     help="run only the single-stream profiling step (for rocprofv3 of the per-kernel numbers)")
     ap.add_argument("--no-host-io", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the strong-scaling and random-regime extras")
+    ap.add_argument("--no-extras", action="store_true", help="skip the strong-scaling, random-regime and ff extras")
+    ap.add_argument("--no-ff", action="store_true", help="skip the force-feedback extra")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="RCCL process group and all-gather even at one process (rehearses RCCL's stream beside "
+                         "the solver's 4 slice streams; DESIGN.md §8)")
     args = ap.parse_args()
     if args.profile_only and args.no_profile:
         ap.error("--profile-only runs only the profiling step: it cannot be combined with --no-profile")
@@ -200,7 +279,7 @@ def main():
         shard.init("gloo", local_rank, world)
         local_rank = 0
     else:
-        shard.init("nccl", local_rank, world)
+        shard.init("nccl", local_rank, world, force=args.force_collective)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
@@ -240,7 +319,7 @@ def main():
     counts = [B] * world
     solver = BatchedBoxFDDP(cfg, max_batch=B, device=local_rank)
     gather = None
-    if world > 1 and args.gather != "none":
+    if (world > 1 or args.force_collective) and args.gather != "none":
         width = shard.pack_results(T, args.gather).shape[1]
         gather = shard.Gatherer(counts, width, dev)
 
@@ -261,10 +340,16 @@ def main():
     iters = T["iters"].cpu().numpy()
     cost = T["cost"].cpu().numpy()
     sb = solve_bytes(stats, nx, nu, N)
-    # whole-job sums over ranks: algorithmic bytes per step, ok count, iterations
+    fp_unit = _profile_json("fp64_latest.json", args.variant, args.contact, B, N)
+    fl = fp64_flops(stats, N, fp_unit)
+    # whole-job sums over ranks: algorithmic bytes per step, ok count, iterations, fp64 flops
     tot = shard.sum_over_ranks(torch.tensor([sb["total"], sb["total_survey_formula"], float(ok.sum()),
-                                             float(iters.sum())], **f64)).cpu().numpy()
-    tot_bytes, tot_survey, tot_ok, tot_it = (float(v) for v in tot)
+                                             float(iters.sum()), fl if fl is not None else -1.0], **f64)).cpu().numpy()
+    tot_bytes, tot_survey, tot_ok, tot_it, tot_fl = (float(v) for v in tot)
+    tot_fl = tot_fl if fl is not None else None
+    unit_counts = {k: float(v) for k, v in zip(("calcdiff", "backward", "trials", "forward_launches"),
+                                           shard.sum_over_ranks(torch.tensor(list(solve_counts(stats).values()),
+                                                                             **f64)).cpu().numpy())}
 
     # ---- per-kernel profiling: the same slice on ONE stream, HIP events
     # around every launch (no overlap between launches) ----
@@ -291,6 +376,12 @@ def main():
         psolver.profile(False)
         pstats = T["stats"].cpu().numpy()
         pb = solve_bytes(pstats, nx, nu, N)
+        pun = solve_units(pstats, N)
+        # the profile times the two line-search passes as two classes; the
+        # PMC per-unit figure is one (k_forward_g8 runs both)
+        pun["forward"] = float(pstats[:, 6].sum()) * (N + 1)
+        pun["forward2"] = float(pstats[:, 7].sum()) * (N + 1)
+        pk64 = fp64_peak_tflops()
         total_ms = sum(v[0] for v in prof.values())
         kernels = {}
         for k, (ms, n) in prof.items():
@@ -302,6 +393,11 @@ def main():
                 bpl = pb[k] * n_prof / n
                 ach = bpl / (ms / n / 1e3) / 1e9
                 e.update({"bytes_per_launch": bpl, "achieved_gbs": ach, "frac": ach / HBM_PEAK_GBS})
+            pu = (fp_unit or {}).get("kernels", {}).get("forward" if k == "forward2" else k, {})
+            if pk64 and "lane_flops_per_unit" in pu and k in pun:
+                fpl = pu["lane_flops_per_unit"] * pun[k] * n_prof / n
+                e.update({"fp64_flops_per_launch": fpl,
+                          "fp64_frac": fpl / (ms / n / 1e3) / 1e12 / pk64})
             kernels[k] = e
         dom = max((k for k in kernels if "achieved_gbs" in kernels[k]), key=lambda k: kernels[k]["ms_per_solve"])
         dominant = dict(name=dom, **kernels[dom])
@@ -310,29 +406,36 @@ def main():
         if args.profile_only:
             if rank == 0:
                 print(json.dumps({"profile_only": True, "kernels": kernels, "dominant": dominant}), flush=True)
-            if world > 1:
+            if dist.is_initialized():
                 dist.destroy_process_group()
             return
 
     value = B * world * args.steps / elapsed
     traffic = pmc_traffic(args.variant, args.contact, B, N) if world == 1 else None
+    hbm, fp = rooflines(tot_bytes, tot_fl, elapsed / args.steps, world)
     roofline = {
-        "bound": "hbm",
+        # the roof this run is closer to: SURVEY §8(d)'s HBM roof, or the
+        # measured fp64 VALU roof that the kernels' issued work is priced
+        # against (the counters show them chain- and issue-bound)
+        "bound": "fp64_valu" if fp is not None and fp["frac"] > hbm["frac"] else "hbm",
         "scope": "whole solve: algorithmic bytes of every kernel (SURVEY.md §8(d) per-node words x device-counted "
                  "calcDiffs / backward passes / line-search launches and step lengths, all ranks) / wall time "
                  "of the timed region",
-        "achieved": tot_bytes * args.steps / elapsed / 1e9,
-        "peak": HBM_PEAK_GBS * world,
+        "achieved": hbm["achieved"],
+        "peak": hbm["peak"],
         "unit": "GB/s",
-        "frac": tot_bytes * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world),
+        "frac": hbm["frac"],
         "traffic": (sum(v for v in traffic.values() if v) if traffic else None),
         "bytes_per_step": tot_bytes,
         "frac_survey_formula": tot_survey * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world),
         "frac_of_measured_copy": tot_bytes * args.steps / elapsed / 1e9 / (HBM_MEASURED_GBS * world),
+        "fp64": None if fp is None else dict(fp, flops_per_step=tot_fl, basis=(
+            "issued fp64 lane-flops (64 x (2 FMA + MUL + ADD) per wave instruction, per node stage / backward node "
+            "/ trial node from tools/pmc_fp64.sh, profiles/fp64_latest.json) x this run's device-counted units, "
+            "over the measured fp64 FMA peak (tools/micro/fp64_peak.hip, profiles/r05_fp64_peak.json)")),
         "dominant_kernel": dominant,
-        # the bound named above is the metric's roofline; the
-        # kernels themselves are limited by their dependent chains (the SQ
-        # counters of this configuration, when profiles/ holds them)
+        # what the SQ counters of this configuration show limits the kernels
+        # (profiles/sq_latest.json, when it is for this configuration)
         "limiter": sq_limiter(args.variant, args.contact, B, N) if world == 1 else None,
     }
     if dominant is not None and traffic and traffic.get(dominant["name"]) is not None:
@@ -350,8 +453,12 @@ def main():
         el = shard.timed_steps(lambda: rsolver.solve_dev(TR, maxiter=args.maxiter, stream=stream), rs, sync)
         rok = float(shard.sum_over_ranks(torch.tensor([float(TR["ok"].sum().item())], **f64)).cpu()[0])
         rit = float(shard.sum_over_ranks(torch.tensor([float(TR["iters"].sum().item())], **f64)).cpu()[0])
+        rstats = TR["stats"].cpu().numpy()
+        rby = float(shard.sum_over_ranks(torch.tensor([solve_bytes(rstats, nx, nu, N)["total"]], **f64)).cpu()[0])
+        rh, _ = rooflines(rby, None, el / rs, world)
         extras["random_regime"] = {"value": B * world * rs / el, "unit": "solves/s", "ms_per_step": el / rs * 1e3,
-                                   "ok_frac": rok / (B * world), "mean_iter": rit / (B * world)}
+                                   "scaling": "weak", "ok_frac": rok / (B * world), "mean_iter": rit / (B * world),
+                                   "roofline": dict(rh, bound="hbm", bytes_per_step=rby)}
         del TR
         if world > 1:
             # strong scaling: rank 0's B-instance batch split into contiguous
@@ -373,10 +480,48 @@ def main():
             sync()
             ss = 3
             el = shard.timed_steps(sstep, ss, sync)
-            extras["strong"] = {"value": B * ss / el, "unit": "solves/s", "global_batch": B,
-                                "batch_per_gpu": scounts, "ms_per_step": el / ss * 1e3}
+            sst = TS["stats"].cpu().numpy()
+            sby = float(shard.sum_over_ranks(torch.tensor([solve_bytes(sst, nx, nu, N)["total"]], **f64)).cpu()[0])
+            sh, _ = rooflines(sby, None, el / ss, world)
+            extras["strong"] = {"metric": METRIC, "value": B * ss / el, "unit": "solves/s", "n_gpus": world,
+                                "steps": ss, "ms_per_step": el / ss * 1e3, "higher_is_better": True,
+                                "scaling": "strong", "global_batch": B, "batch_per_gpu": scounts,
+                                "roofline": dict(sh, bound="hbm", bytes_per_step=sby),
+                                "note": "one B-instance batch split into contiguous B/G slices (SURVEY §8(e)); "
+                                        "the headline gives every GPU its own B-instance shard (weak)"}
             ssolver.close()
             del TS
+        if not args.no_ff and args.variant == "classical":
+            # the force-feedback variant (configs[2]'s model, nx = 21) at the
+            # metric's batch and horizon: every rank its own B-instance shard
+            fcfg = ff_preset(N, args.contact)
+            fb = workload.make_batch(B, N, "ff", _abi.gravity_torque, ee, seed=SEED + 2 + rank, regime=args.regime,
+                                     fk=_abi.frame_placement)
+            TF = tensors(fb)
+            for k, shp in (("xs", (B, N + 1, 21)), ("K", (B, N, nu, 21))):
+                TF[k] = torch.zeros(shp, **f64)
+            fsolver = BatchedBoxFDDP(fcfg, max_batch=B, device=local_rank)
+            fsolver.solve_dev(TF, maxiter=args.maxiter, stream=stream)
+            sync()
+            fs_ = 3
+            el = shard.timed_steps(lambda: fsolver.solve_dev(TF, maxiter=args.maxiter, stream=stream), fs_, sync)
+            fst = TF["stats"].cpu().numpy()
+            fok = float(shard.sum_over_ranks(torch.tensor([float(TF["ok"].sum().item())], **f64)).cpu()[0])
+            fit = float(shard.sum_over_ranks(torch.tensor([float(TF["iters"].sum().item())], **f64)).cpu()[0])
+            fby = float(shard.sum_over_ranks(torch.tensor([solve_bytes(fst, 21, nu, N)["total"]], **f64)).cpu()[0])
+            ffl = fp64_flops(fst, N, _profile_json("fp64_latest_ff.json", "ff", args.contact, B, N))
+            if ffl is not None:
+                ffl = float(shard.sum_over_ranks(torch.tensor([ffl], **f64)).cpu()[0])
+            fh, ffp = rooflines(fby, ffl, el / fs_, world)
+            extras["ff"] = {"value": B * world * fs_ / el, "unit": "solves/s", "ms_per_step": el / fs_ * 1e3,
+                            "scaling": "weak", "workload": f"ForceFeedback (q,v,tau_hat)/w nx=21 nu=7, horizon={N}, "
+                                                          f"batch={B} per GPU, maxiter={args.maxiter}, "
+                                                          f"contact={args.contact}",
+                            "ok_frac": fok / (B * world), "mean_iter": fit / (B * world),
+                            "roofline": dict(fh, bound="fp64_valu" if ffp and ffp["frac"] > fh["frac"] else "hbm",
+                                             bytes_per_step=fby, fp64=ffp)}
+            fsolver.close()
+            del TF
 
     host_io = None
     if not args.no_host_io and world == 1:
@@ -443,6 +588,7 @@ def main():
             },
             "roofline": roofline,
             "cpu_baseline": base,
+            "counts_per_step": unit_counts,
             "solver": {
                 "ok_frac": tot_ok / (B * world),
                 "mean_iter": tot_it / (B * world),
@@ -456,7 +602,7 @@ def main():
             **extras,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -518,7 +518,7 @@ template <bool FF> struct BwW {
   static constexpr int REC = rec_words(NX);
   double R[(REC + 63) / 64 * 64];  // staged node record (A | Lxx | Lxu | Luu | Lx | Lu | cost | lam), padded
   double V[NX * NX];  // V_xx' on entry to a node, V_xx on exit
-  double Q[ND * ND];  // [[Qxx, Qxu], [Qux, Quu + preg I]]
+  double Q[ND * ND + 1];  // [[Qxx, Qxu], [Qux, Quu + preg I]]; Q[ND * ND]: phase C's spare lanes store here
   double W[NX * NU];  // V D
   double Y[NU * NU];  // D' V D
   double M[ND * NU];
@@ -796,8 +796,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 #pragma unroll
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
-    if (l + 64 * k < NQE) tri_rc(l + 64 * k, r, c);
-    qrc[k] = (r << 8) | c;
+    const bool spare = l + 64 * k >= NQE;  // past the last entry: computes entry (0, 0), stores to Q[ND * ND]
+    if (!spare) tri_rc(l + 64 * k, r, c);
+    qrc[k] = (spare ? 1 << 16 : 0) | (r << 8) | c;
   }
 #pragma unroll
   for (int k = 0; k < NVL; ++k) {
@@ -919,11 +920,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       // ---- phase C: Q lower triangle (mirrored), entries fixed per lane ----
 #pragma unroll QC_N
       for (int k = 0; k < NQL; ++k) {
-        // no range guard: a lane past the last entry holds entry (0, 0)
-        // (qrc's default) and writes the same bits as the lane that owns it,
-        // so the passes need no divergent branch and can interleave
+        // no range guard: a lane past the last entry computes entry (0, 0)
+        // (qrc's default) and stores it to the spare slot Q[ND * ND] (the
+        // address is selected, not the branch), so the passes need no
+        // divergent branch and can interleave, and no entry has two writers
         {
-          const int r = qrc[k] >> 8, c = qrc[k] & 255;
+          const int r = (qrc[k] >> 8) & 255, c = qrc[k] & 255;
+          const bool spare = (qrc[k] >> 16) != 0;
           double lv;
           if (r < NX)
             lv = S.R[rec_off_Lxx(NX) + r * NX + c];
@@ -947,8 +950,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-          S.Q[r * ND + c] = v;
-          S.Q[c * ND + r] = v;
+          S.Q[spare ? ND * ND : r * ND + c] = v;
+          S.Q[spare ? ND * ND : c * ND + r] = v;
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
@@ -1188,8 +1191,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
-    if (tid + 128 * k < NQE) tri_rc(tid + 128 * k, r, c);
-    qrc[k] = (r << 8) | c;
+    const bool spare = tid + 128 * k >= NQE;  // past the last entry: computes entry (0, 0), stores to Q[ND * ND]
+    if (!spare) tri_rc(tid + 128 * k, r, c);
+    qrc[k] = (spare ? 1 << 16 : 0) | (r << 8) | c;
   }
 #pragma unroll
   for (int k = 0; k < NVL; ++k) {
@@ -1378,11 +1382,13 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // ---- phase C: Q lower triangle (mirrored), entries over 128 lanes ----
 #pragma unroll
       for (int k = 0; k < NQL; ++k) {
-        // no range guard: a lane past the last entry holds entry (0, 0)
-        // (qrc's default) and writes the same bits as the lane that owns it,
-        // so the passes need no divergent branch and can interleave
+        // no range guard: a lane past the last entry computes entry (0, 0)
+        // (qrc's default) and stores it to the spare slot Q[ND * ND] (the
+        // address is selected, not the branch), so the passes need no
+        // divergent branch and can interleave, and no entry has two writers
         {
-          const int r = qrc[k] >> 8, c = qrc[k] & 255;
+          const int r = (qrc[k] >> 8) & 255, c = qrc[k] & 255;
+          const bool spare = (qrc[k] >> 16) != 0;
           double lv;
           if (r < NX)
             lv = S.R[rec_off_Lxx(NX) + r * NX + c];
@@ -1406,8 +1412,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-          S.Q[r * ND + c] = v;
-          S.Q[c * ND + r] = v;
+          S.Q[spare ? ND * ND : r * ND + c] = v;
+          S.Q[spare ? ND * ND : c * ND + r] = v;
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
@@ -2245,6 +2251,13 @@ struct ffddp_handle {
   // per-iteration trace (ffddp_trace_enable)
   double* trace = nullptr;
   int trace_it = 0;
+  // live solve plans (their graphs captured this handle's workspace and
+  // trace pointer): ffddp_trace_enable refuses while any is alive and
+  // ffddp_destroy invalidates them; last_done marks the end of the last
+  // solve_batch[_dev] call, which ffddp_plan_run waits for on the device
+  std::vector<ffddp_plan*> plans;
+  hipEvent_t last_done = nullptr;
+  bool last_done_set = false;
   // sub-batch streams: the batch is split into nstreams slices solved on their
   // own HIP streams, so latency-bound phases of one slice overlap with the
   // throughput-bound phases of another (FFDDP_STREAMS, default 4: three
@@ -2831,9 +2844,14 @@ int ffddp_profile_read(ffddp_handle* h, double* ms, int64_t* launches, int reset
   return 0;
 }
 
+static void plan_invalidate(ffddp_plan* p);
+
 void ffddp_destroy(ffddp_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
+  for (ffddp_plan* p : h->plans) plan_invalidate(p);
+  h->plans.clear();
+  if (h->last_done) (void)hipEventDestroy(h->last_done);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->sev) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->stg) (void)hipEventDestroy(e);
@@ -2844,6 +2862,15 @@ void ffddp_destroy(ffddp_handle* h) {
 }
 
 const char* ffddp_last_error(const ffddp_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+// the end of the solve just enqueued on stream s (every slice has joined s),
+// for ffddp_plan_run to wait on
+static int mark_solve_done(ffddp_handle* h, hipStream_t s) {
+  if (!h->last_done) HIPCHK(h, hipEventCreateWithFlags(&h->last_done, hipEventDisableTiming));
+  HIPCHK(h, hipEventRecord(h->last_done, s));
+  h->last_done_set = true;
+  return 0;
+}
 
 int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double* node_ref, const double* inst_ref,
                           const uint8_t* surface, const double* xs_init, const double* us_init, int maxiter,
@@ -2856,8 +2883,10 @@ int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double
   if (!x0 || !node_ref || !inst_ref || !surface || !xs_init || !us_init || !xs || !us || !K || !cost || !iters || !ok)
     return fail(h, FFDDP_E_INVALID, "null pointer");
   HIPCHK(h, hipSetDevice(h->device));
-  return launch_solve(h, B, x0, node_ref, inst_ref, surface, xs_init, us_init, maxiter, is_feasible, xs, us, K,
-                      cost, iters, ok, fn_pred, stats, (hipStream_t)stream);
+  const int rc = launch_solve(h, B, x0, node_ref, inst_ref, surface, xs_init, us_init, maxiter, is_feasible, xs, us,
+                              K, cost, iters, ok, fn_pred, stats, (hipStream_t)stream);
+  if (rc) return rc;
+  return mark_solve_done(h, (hipStream_t)stream);
 }
 
 // error exit of the host entry point after its first asynchronous copy: the
@@ -2979,7 +3008,8 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
 // call -- the receding-horizon loop's one solve per control tick
 // ---------------------------------------------------------------------------
 struct ffddp_plan {
-  ffddp_handle* h = nullptr;
+  ffddp_handle* h = nullptr;  // null once the handle is destroyed (plan_invalidate)
+  int device = 0;
   int B = 0;
   hipStream_t s = nullptr;
   hipGraphExec_t ge = nullptr;
@@ -3047,6 +3077,7 @@ int ffddp_plan_create(ffddp_handle* h, int B, int maxiter, int is_feasible, ffdd
   ffddp_plan* p = new (std::nothrow) ffddp_plan();
   if (!p) return fail(h, FFDDP_E_OOM, "plan allocation failed");
   p->h = h;
+  p->device = h->device;
   p->B = B;
   p->in_bytes = L.in_bytes;
   p->out_bytes = L.out_bytes;
@@ -3111,23 +3142,45 @@ int ffddp_plan_create(ffddp_handle* h, int B, int maxiter, int is_feasible, ffdd
   io->ok = (const uint8_t*)(ho + L.ok);
   io->fn_pred = (const double*)(ho + L.fn);
   io->stats = (const int32_t*)(ho + L.stats);
+  h->plans.push_back(p);
   *out = p;
   return 0;
 }
 
 int ffddp_plan_run(ffddp_plan* p) {
-  if (!p) return FFDDP_E_INVALID;
+  if (!p || !p->h || !p->ge) return FFDDP_E_INVALID;  // null, or its handle was destroyed
   ffddp_handle* h = p->h;
   HIPCHK(h, hipSetDevice(h->device));
+  // the graph works in the handle's workspace: after a solve still running
+  // on another stream (solve_batch_dev is asynchronous), never beside it
+  if (h->last_done_set) HIPCHK(h, hipStreamWaitEvent(p->s, h->last_done, 0));
   HIPCHK(h, hipGraphLaunch(p->ge, p->s));
   HIPCHK(h, hipStreamSynchronize(p->s));
   return 0;
 }
 
+// the handle is going away: drop the graph (it references the handle's
+// workspace); the page-locked io arrays and the device buffers stay until
+// ffddp_plan_destroy
+static void plan_invalidate(ffddp_plan* p) {
+  (void)hipStreamSynchronize(p->s);
+  if (p->ge) (void)hipGraphExecDestroy(p->ge);
+  p->ge = nullptr;
+  p->h = nullptr;
+}
+
 void ffddp_plan_destroy(ffddp_plan* p) {
   if (!p) return;
-  (void)hipSetDevice(p->h->device);
+  (void)hipSetDevice(p->device);
   (void)hipStreamSynchronize(p->s);
+  if (p->h) {
+    std::vector<ffddp_plan*>& v = p->h->plans;
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i] == p) {
+        v.erase(v.begin() + (long)i);
+        break;
+      }
+  }
   plan_free(p);
 }
 
@@ -3196,6 +3249,9 @@ int ffddp_set_solver_params(ffddp_handle* h, const ffddp_solver_params* p) {
 
 int ffddp_trace_enable(ffddp_handle* h, int max_iters) {
   if (!h || max_iters < 0) return FFDDP_E_INVALID;
+  // a live plan's graph writes the trace buffer it captured (or none)
+  if (!h->plans.empty())
+    return fail(h, FFDDP_E_INVALID, "solve plans of this handle are alive: destroy them before ffddp_trace_enable");
   HIPCHK(h, hipSetDevice(h->device));
   if (h->trace) {
     HIPCHK(h, hipDeviceSynchronize());

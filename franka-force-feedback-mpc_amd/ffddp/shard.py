@@ -32,9 +32,19 @@ def env_ranks():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str, local_rank: int, world: int):
-    """Process group for world > 1 (MASTER_ADDR defaults to 127.0.0.1)."""
+def init(backend: str, local_rank: int, world: int, force: bool = False):
+    """Process group for world > 1 (MASTER_ADDR defaults to 127.0.0.1).
+    force: a one-process group as well (an in-memory store), so that one GPU
+    can rehearse the RCCL all-gather and its stream beside the solver's."""
+    if world <= 1 and not force:
+        return
     if world <= 1:
+        kw = dict(store=dist.HashStore(), rank=0, world_size=1)
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), **kw)
+        else:
+            dist.init_process_group(backend, **kw)
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend == "nccl":
@@ -98,7 +108,7 @@ class Gatherer:
 
     def __call__(self, local: torch.Tensor) -> torch.Tensor:
         n = local.shape[0]
-        if self.world == 1:
+        if self.world == 1 and not dist.is_initialized():
             return local
         self.send[:n].copy_(local)
         if dist.get_backend() == "nccl":

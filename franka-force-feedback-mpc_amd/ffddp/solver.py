@@ -17,6 +17,7 @@ per-iteration record of instance 0 after each solve (ffddp.callbacks).
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import numpy as np
 
@@ -44,6 +45,7 @@ class BatchedBoxFDDP:
         self._pin = {}
         self._callbacks = []
         self._trace_it = 0
+        self._plans = weakref.WeakSet()  # live SolvePlans: closed before the handle
         self.N = int(cfg.horizon)
         self.nx = cfg.nx
         self.nu = 7
@@ -95,6 +97,8 @@ class BatchedBoxFDDP:
         return list(self._callbacks)
 
     def trace_enable(self, max_iters: int):
+        """Fails (FfddpError) while a SolvePlan of this solver is open: a
+        plan's graph keeps the trace buffer it was captured with."""
         self._check(self._lib.ffddp_trace_enable(self._h, int(max_iters)), "ffddp_trace_enable")
         self._trace_it = int(max_iters)
 
@@ -116,6 +120,8 @@ class BatchedBoxFDDP:
 
     # -- lifecycle ------------------------------------------------------------------
     def close(self):
+        for plan in list(getattr(self, "_plans", ())):
+            plan.close()
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.ffddp_destroy(self._h)
             self._h = None
@@ -186,7 +192,9 @@ class BatchedBoxFDDP:
     def plan(self, B: int, maxiter: int = 10, is_feasible: bool = False) -> "SolvePlan":
         """ffddp_plan_create: the host-array solve of B instances captured as one
         HIP graph; see SolvePlan."""
-        return SolvePlan(self, B, maxiter, is_feasible)
+        plan = SolvePlan(self, B, maxiter, is_feasible)
+        self._plans.add(plan)
+        return plan
 
     # -- solve (device-resident torch tensors; bench path) ---------------------------
     def solve_dev(self, t, maxiter: int = 10, is_feasible: bool = False, stream=None):
@@ -318,6 +326,8 @@ class SolvePlan:
     def run(self) -> np.ndarray:
         if self._h is None:
             raise FfddpError("plan closed")
+        if self.solver._h is None:
+            raise FfddpError("the plan's solver is closed")
         self.solver._check(self._lib.ffddp_plan_run(self._h), "ffddp_plan_run")
         self.solver._run_callbacks(self.B)
         return self.ok
@@ -326,6 +336,9 @@ class SolvePlan:
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.ffddp_plan_destroy(self._h)
         self._h = None
+        plans = getattr(getattr(self, "solver", None), "_plans", None)
+        if plans is not None:
+            plans.discard(self)
 
     def __del__(self):
         try:

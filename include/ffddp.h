@@ -184,9 +184,15 @@ int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double
  * *io: refill the inputs in place before each run, read the outputs after it
  * (overwritten by the next run).  Results equal ffddp_solve_batch's bit for
  * bit.  The solver properties (ffddp_set_solver_params) apply to later runs;
- * tracing and per-kernel timing are fixed at creation (timing off).  A plan
- * uses its handle's workspace: destroy plans before their handle, and do not
- * run a plan concurrently with another solve of the same handle. */
+ * tracing and per-kernel timing are fixed at creation (timing off):
+ * ffddp_trace_enable returns FFDDP_E_INVALID while a plan of the handle is
+ * alive.  A plan uses its handle's workspace.  ffddp_plan_run first waits (on
+ * the device) for the handle's last solve_batch[_dev] call to finish, on
+ * whatever stream it ran; do not run a plan from a second host thread while
+ * another solve of the same handle is being enqueued.  ffddp_destroy
+ * invalidates the handle's live plans: their ffddp_plan_run then returns
+ * FFDDP_E_INVALID, and ffddp_plan_destroy still frees them (their io arrays
+ * stay valid until then). */
 typedef struct ffddp_plan ffddp_plan;
 typedef struct ffddp_plan_io {
   double* x0;        /* [B][nx]        inputs, written by the caller */

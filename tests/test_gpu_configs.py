@@ -145,3 +145,48 @@ def test_c5_per_gpu_shape_point3d_n100(monkeypatch):
     assert max(e["xs"], e["us"], e["cost"]) < 1e-9 and e["K"] < 1e-9 and e["K_elem"] < 2e-7, e
     big.close()
     small.close()
+
+
+def test_c5_whole_workload_point3d_n100_b8192(monkeypatch):
+    """configs[4] as its whole workload on one GPU: 8192 instances, horizon
+    100, point3d (ContactModel3D, crocoddyl_classical.py:944-966).  The node
+    records alone are 8192 x 101 x 528 x 8 B = 3.5 GB, so every device buffer
+    offset past 2^31 bytes is exercised.  Instances spread over the whole
+    batch (the last slice included) equal the same instances solved 8 at a
+    time on one stream, bit for bit, and a spread of them matches the
+    oracle at the C5 tolerances."""
+    N, B = 100, 8192
+    cfg = product_cfg("classical", N, "point3d")
+    batch = make_batch("classical", B, N, seed=808, surface=1)
+    big = BatchedBoxFDDP(cfg, max_batch=B)
+    big.solve(batch, maxiter=10)
+    assert np.all(np.isfinite(big.cost)) and np.all(np.isfinite(big.K))
+    assert float(np.mean(big.ok)) > 0.5
+    monkeypatch.setenv("FFDDP_STREAMS", "1")
+    small = BatchedBoxFDDP(cfg, max_batch=8)
+    rng = np.random.default_rng(3)
+    picks = np.unique(np.concatenate([[0, B // 4 - 1, B // 4, B // 2 + 1, 3 * B // 4, B - 2, B - 1],
+                                      rng.integers(0, B, 9)]))
+    for i0 in range(0, len(picks), 8):
+        idx = picks[i0:i0 + 8]
+        small.solve(_sub(batch, idx), maxiter=10)
+        for j, i in enumerate(idx):
+            for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred", "stats"):
+                a, b = getattr(big, name)[i], getattr(small, name)[j]
+                assert np.array_equal(a, b, equal_nan=True), (name, int(i))
+    sel = picks[::3]
+    from oracle import fddp
+
+    ref = solve_many(cfg, batch, sel, consts=fddp.Consts(gains_form="solve"))
+    e = dict(xs=0.0, us=0.0, K=0.0, cost=0.0, K_elem=0.0)
+    for i, r in zip(sel, ref):
+        assert bool(big.ok[i]) == r["ok"] and int(big.iter[i]) == r["iter"]
+        assert int(big.stats[i, 1]) == r["trials"]
+        for k in ("xs", "us", "K"):
+            e[k] = max(e[k], rel_err(getattr(big, k)[i], r[k]))
+        e["cost"] = max(e["cost"], rel_err(big.cost[i], r["cost"]))
+        e["K_elem"] = max(e["K_elem"], elem_err(big.K[i], r["K"]))
+    log_parity(f"batch/point3d/N{N}/B{B}/solve_form", n=len(sel), **e)
+    assert max(e["xs"], e["us"], e["cost"]) < 1e-9 and e["K"] < 1e-9 and e["K_elem"] < 2e-7, e
+    big.close()
+    small.close()

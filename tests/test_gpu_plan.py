@@ -10,7 +10,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from ffddp import BatchedBoxFDDP, FfddpError
+from ffddp import BatchedBoxFDDP, FfddpError, _abi
 
 from helpers import make_batch, product_cfg
 
@@ -63,4 +63,58 @@ def test_plan_solver_params_and_errors():
     with pytest.raises(FfddpError):
         s.plan(B + 1)
     s.close()
+    ref.close()
+
+
+def test_plan_lifetime_rules():
+    """a plan's graph holds the handle's workspace and trace
+    pointer.  Tracing cannot change while a plan is alive; closing the solver
+    closes its plans first (no dangling handle); a plan's run after an
+    asynchronous device solve on another stream waits for it."""
+    import torch
+
+    N, B = 30, 8
+    cfg = product_cfg("classical", N)
+    batch = make_batch("classical", B, N, seed=7)
+    s = BatchedBoxFDDP(cfg, max_batch=B)
+    ref = BatchedBoxFDDP(cfg, max_batch=B)
+    plan = s.plan(B, maxiter=10)
+    with pytest.raises(FfddpError, match="plans"):
+        s.trace_enable(8)
+    with pytest.raises(FfddpError):
+        s.setCallbacks([lambda solver, tr: None])
+    plan.close()
+    s.trace_enable(8)  # no live plan: allowed again
+    s.trace_enable(0)
+
+    # device solve on a side stream, then the plan in program order: the
+    # plan's graph waits for it on the device, so both results stay exact
+    dev = torch.device("cuda", 0)
+    f64 = dict(dtype=torch.float64, device=dev)
+    other = make_batch("classical", B, N, seed=8)
+    t = dict(x0=torch.tensor(other.x0, **f64), node_ref=torch.tensor(other.node_ref, **f64),
+             inst_ref=torch.tensor(other.inst_ref, **f64),
+             surface=torch.tensor(other.surface, dtype=torch.uint8, device=dev),
+             xs_init=torch.tensor(other.xs_init, **f64), us_init=torch.tensor(other.us_init, **f64),
+             xs=torch.zeros((B, N + 1, 14), **f64), us=torch.zeros((B, N, 7), **f64),
+             K=torch.zeros((B, N, 7, 14), **f64), cost=torch.zeros(B, **f64),
+             iters=torch.zeros(B, dtype=torch.int32, device=dev), ok=torch.zeros(B, dtype=torch.uint8, device=dev),
+             fn_pred=torch.zeros((B, 2), **f64),
+             stats=torch.zeros((B, _abi.NSTATS), dtype=torch.int32, device=dev))
+    side = torch.cuda.Stream(dev)
+    plan = s.plan(B, maxiter=10)
+    plan.fill(batch)
+    s.solve_dev(t, maxiter=10, stream=side.cuda_stream)
+    plan.run()
+    torch.cuda.synchronize(dev)
+    ref.solve(batch, maxiter=10)
+    _same(ref, plan, "plan after side-stream solve")
+    ref.solve(other, maxiter=10)
+    assert np.array_equal(t["xs"].cpu().numpy(), ref.xs) and np.array_equal(t["K"].cpu().numpy(), ref.K)
+
+    # closing the solver closes the plan first; the plan then refuses to run
+    s.close()
+    with pytest.raises(FfddpError):
+        plan.run()
+    plan.close()  # idempotent
     ref.close()

@@ -128,3 +128,31 @@ def test_single_rank_passthrough():
     local = shard.pack_results(res, "costs")
     assert local.shape == (3, 10)
     assert torch.equal(shard.Gatherer([3], 10, "cpu")(local), local)
+
+
+def _forced_worker(q):
+    sys.path.insert(0, str(ROOT))
+    import ffddp_path  # noqa: F401
+    from ffddp import shard
+
+    shard.init("gloo", 0, 1, force=True)  # bench --force-collective at one process
+    try:
+        assert dist.is_initialized() and dist.get_world_size() == 1
+        local = torch.arange(12, dtype=torch.float64).reshape(3, 4)
+        g = shard.Gatherer([3], 4, torch.device("cpu"))
+        out = g(local)
+        # the collective ran (the gather went through the process group's
+        # buffers, not the one-process shortcut) and kept the rows
+        q.put((bool(torch.equal(out, local)), bool(torch.equal(g.recv[0], local))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_forced_one_process_group():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(q,))
+    p.start()
+    p.join(120)
+    assert p.exitcode == 0
+    assert q.get(timeout=5) == (True, True)

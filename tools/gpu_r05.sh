@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-5 GPU steps named in $STEPS, each under its own time limit, stopping
+# at the first failure.
+#   peak    measured fp64 FMA throughput (tools/micro/fp64_peak, built on the CPU host)
+#   fp64    fp64 PMC pass per kernel class, classical B=4096 and FF B=4096 (tools/pmc_fp64.sh)
+#   bits    in-tree library vs lib/base bit for bit (tools/lib_dump.py)
+#   nccl    one-process RCCL group: bench at B=4096 / 512 with --gather none / costs / full
+#   tests   pytest -m gpu with the parity log
+#   bench   one default bench line
+#   quick   short bench lines at B = 4096 / 1024 / 512 (no extras)
+# usage: [STEPS="tests bench"] tools/gpu_r05.sh TAG
+set -e
+R=${GRAFT_REPO_ROOT:-/root/repo}
+TAG=${1:-r05}
+O=$R/gpurun_out/$TAG; mkdir -p $O
+cd $R
+STEPS=${STEPS:-"peak fp64 tests bench"}
+for st in $STEPS; do
+  case $st in
+    peak) timeout -k 10 60 tools/micro/fp64_peak > $O/fp64_peak.txt 2>&1; cat $O/fp64_peak.txt ;;
+    fp64) BENCH_ARGS="--batch 4096" $R/tools/pmc_fp64.sh $TAG/fp4096 > $O/fp.log 2>&1; cat $O/fp.log
+          BENCH_ARGS="--batch 4096 --variant ff" FP_CONFIG=ff/normal_1d/B4096/N30 $R/tools/pmc_fp64.sh $TAG/fpff > $O/fpff.log 2>&1; cat $O/fpff.log ;;
+    bits) FFDDP_LIB=$R/franka-force-feedback-mpc_amd/lib/base/libffddp.so timeout -k 10 200 python3 tools/lib_dump.py $O/a.npz > $O/dump_a.log 2>&1
+          timeout -k 10 200 python3 tools/lib_dump.py $O/b.npz > $O/dump_b.log 2>&1
+          python3 tools/lib_dump.py --compare $O/a.npz $O/b.npz | tee $O/bits.txt; rm -f $O/a.npz $O/b.npz ;;
+    nccl) for B in 4096 512; do for g in none costs full; do
+            timeout -k 10 200 python3 bench.py --batch $B --force-collective --gather $g --steps 20 --warmup 3 \
+              --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/nccl_${B}_$g.log 2>&1 || { tail -20 $O/nccl_${B}_$g.log; exit 1; }
+            python3 -c "import json; d=json.loads(open('$O/nccl_${B}_$g.log').read().strip().splitlines()[-1]); print($B, '$g', round(d['value']), 'ms/step %.3f' % d['ms_per_step'])" | tee -a $O/nccl.txt
+          done; done ;;
+    tests) rm -f $O/parity.jsonl
+        FFDDP_PARITY_LOG=$O/parity.jsonl timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+          --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
+        tail -1 $O/gpu_tests.log ;;
+    bench) timeout -k 10 400 python3 bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+        tail -1 $O/bench.log | cut -c1-300 ;;
+    quick) for B in 4096 1024 512; do
+        timeout -k 10 200 python3 bench.py --batch $B --no-cpu-baseline --no-extras --no-host-io > $O/q_$B.log 2>&1 || { tail -20 $O/q_$B.log; exit 1; }
+        python3 -c "import json; d=json.loads(open('$O/q_$B.log').read().strip().splitlines()[-1]); k=d['kernels']; print($B, round(d['value']), 'ms/step %.2f'%d['ms_per_step'], ' '.join('%s=%.0f'%(n,v['avg_launch_ms']*1e3) for n,v in k.items()))"
+      done ;;
+  esac
+  echo "step $st done"
+done
