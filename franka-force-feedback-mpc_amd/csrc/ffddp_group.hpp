@@ -201,6 +201,19 @@ __device__ __forceinline__ void lane_consts_fill(const DevConsts& C, LaneK* LK, 
   k.wslim = C.ws_lim[j];
 }
 
+// ROW line-search layout (ffddp_rollout.hpp): lanes 8..15 of the block fill
+// LK[8..15], the phantom group of each DPP row: the joint frames of lanes
+// 0..7 (finite kinematics) with zero mass, inertia and centre of mass, so its
+// link forces and CRBA tuples are exact zeros in the real group's suffix sums
+__device__ __forceinline__ void lane_consts_fill_phantom(const DevConsts& C, LaneK* LK, int li16) {
+  if (li16 < G8 || li16 >= 2 * G8) return;
+  lane_consts_fill(C, LK + G8, li16 - G8);
+  LaneK& k = LK[li16];
+  k.m = 0.0;
+  for (int e = 0; e < 9; ++e) k.I[e] = 0.0;
+  for (int e = 0; e < 3; ++e) k.com[e] = 0.0;
+}
+
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* c) {
   c[0] = a[1] * b[2] - a[2] * b[1];
   c[1] = a[2] * b[0] - a[0] * b[2];

@@ -41,6 +41,7 @@
 #include "ffddp_group.hpp"
 #include "ffddp_plant.hpp"
 #include "ffddp_primal_g8.hpp"
+#include "ffddp_rollout.hpp"
 
 using namespace ffddp;
 
@@ -1695,17 +1696,30 @@ __device__ __forceinline__ int first_width(int n1, const Dev& d, int cur, int wi
 
 // one wave per SIMD: the register budget holds the next node's K row,
 // prefetched one node ahead (a 2-waves/SIMD variant without the prefetch
-// measured slower in every iteration)
-template <int NC, bool FF>
+// measured slower in every iteration).
+// ROW (ffddp_rollout.hpp): one trial group per 16-lane DPP row (latency
+// layout) instead of two (throughput layout).  Both instantiations are
+// launched for a pass whose layout the host cannot know; each reads the
+// slice's active count and returns at once unless it is the chosen one:
+// ROW while the pass's trial groups fit row_max (one wave per SIMD share at
+// four groups per wave).  The two give the same bits, so the choice never
+// makes a result depend on the batch.  The node loop is written with
+// explicit fma under fp contract(off) for that reason.
+__device__ __forceinline__ int ls_row_bcast0(int v) {  // lane 0 of the row into every lane of it
+  return __builtin_amdgcn_update_dpp(v, v, 0x150, 0xf, 0xf, false);
+}
+#pragma clang fp contract(off)
+template <int NC, bool FF, bool ROW>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_forward_g8(const DevConsts* __restrict__ Cg, Dev d,
                                                    const double* __restrict__ x0,
                                                    const double* __restrict__ node_ref,
                                                    const double* __restrict__ inst_ref,
                                                    const uint8_t* __restrict__ surface, int tr0, int ntr,
-                                                   int only_more, int cur, int wide_max) {
+                                                   int only_more, int cur, int wide_max, int row_max) {
   const DevConsts& C = *Cg;
   const int N = C.N;
   constexpr int nx = FF ? 21 : 14;
+  constexpr int GL = ROW ? 16 : G8;  // lanes per trial group slot
   // host: first pass (0, n1), second pass (n1, NTRIALS - n1); the device may
   // widen the first pass to all step lengths (first_width)
   {
@@ -1713,17 +1727,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
     tr0 = only_more ? n1 : 0;
     ntr = only_more ? NTRIALS - n1 : n1;
     if (ntr == 0) return;
+    // the layout of this pass (same decision in both instantiations)
+    if (((long)d.acnt[cur] * ntr <= (long)row_max) != ROW) return;
   }
-  const long blk = xcd_block(blockIdx.x, ((long)d.acnt[cur] * ntr * G8 + 63) / 64);
-  const long gid = (blk * (long)blockDim.x + threadIdx.x) / G8;
+  const long blk = xcd_block(blockIdx.x, ((long)d.acnt[cur] * ntr * GL + 63) / 64);
+  const long gid = (blk * (long)blockDim.x + threadIdx.x) / GL;
   const int li = g8_lane();
   const bool J = li < NQ;
   const int ji = J ? li : 0;
+  const bool real = !ROW || (threadIdx.x & 8) == 0;  // ROW: lanes 8..15 of a row are the phantom group
+  const bool Js = J && real;                          // stores
   const int slot = (int)(gid / ntr), tr = tr0 + (int)(gid % ntr);
-  __shared__ LaneK LKs[G8];
+  __shared__ LaneK LKs[ROW ? 16 : G8];
   lane_consts_fill(C, LKs, (int)threadIdx.x);
+  if (ROW) lane_consts_fill_phantom(C, LKs, (int)threadIdx.x);
   __syncthreads();
-  const LaneK& K = LKs[li];
+  const LaneK& K = LKs[ROW ? (threadIdx.x & 15) : li];
   const ActiveList al = active_list(d, cur);
   if (slot >= al.n) return;
   const int b = al.list[slot];
@@ -1794,12 +1813,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
     double xq_t = hq, xv_t = hv, xt_t = ht;
     const double sq = pxs[0], sv = pxs[1], stt = pxs[2];
     if (gap) {
-      xq_t = hq + pfs[0] * (alpha - 1.0);
-      xv_t = hv + pfs[1] * (alpha - 1.0);
-      if (FF) xt_t = ht + pfs[2] * (alpha - 1.0);
+      xq_t = fma(pfs[0], alpha - 1.0, hq);
+      xv_t = fma(pfs[1], alpha - 1.0, hv);
+      if (FF) xt_t = fma(pfs[2], alpha - 1.0, ht);
     }
-    if (!feas) dvp -= pw[0] * (sq - xq_t) + pw[1] * (sv - xv_t) + (FF ? pw[2] * (stt - xt_t) : 0.0);
-    if (J) {
+    if (!feas) {
+      dvp = fma(-pw[0], sq - xq_t, dvp);
+      dvp = fma(-pw[1], sv - xv_t, dvp);
+      if (FF) dvp = fma(-pw[2], stt - xt_t, dvp);
+    }
+    if (Js) {
       xtr[(long)t * nx + ji] = xq_t;
       xtr[(long)t * nx + 7 + ji] = xv_t;
       if (FF) xtr[(long)t * nx + 14 + ji] = xt_t;
@@ -1808,48 +1831,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
 #pragma unroll
     for (int c = 0; c < 6; ++c) ref[c] = pref[c];
     if (t < N) {
-      // u_i = us_i - alpha k_i - K_i (x - xs)
+      // u_i = us_i - alpha k_i - K_i (x - xs)  (crocoddyl order: x components q, v, tau)
       double u = 0.0;
       {
-        double acc = pus - pk * alpha;
+        double acc = fma(-pk, alpha, pus);
         const double dq = xq_t - sq, dv = xv_t - sv, dtt = xt_t - stt;
 #pragma unroll
         for (int m = 0; m < NQ; ++m) {
-          const double dqm = g8_get(dq, m), dvm = g8_get(dv, m);
-          acc -= pK[m] * dqm;
-          acc -= pK[7 + m] * dvm;
-          if (FF) acc -= pK[14 + m] * g8_get(dtt, m);
+          const double dqm = ls_get<ROW>(dq, m), dvm = ls_get<ROW>(dv, m);
+          acc = fma(-pK[m], dqm, acc);
+          acc = fma(-pK[7 + m], dvm, acc);
+          if (FF) acc = fma(-pK[14 + m], ls_get<ROW>(dtt, m), acc);
         }
-        // crocoddyl order: sum over x components 0..nx-1 (q then v then tau); rounding-level difference only
         if (C.use_box) acc = fmin(fmax(acc, K.ulb), K.uub);
         u = acc;
-        if (J) utr[(long)t * NU + ji] = u;
+        if (Js) utr[(long)t * NU + ji] = u;
       }
       fetch(t + 1);
       double qn, vn, cp, lam[3];
       const double uin = FF ? xt_t : u;
       PP(8);
-      node_calc_g8<NC>(C, K, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam
+      ls_node_calc<NC, ROW>(C, K, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam
 #ifdef FFDDP_PHASE_PROF
-                       , pp_acc, pp_last
+                            , pp_acc, pp_last
 #endif
       );
       double c = C.dt * cp;
       double tn = 0.0;
       if (FF) {
-        tn = C.alpha * xt_t + C.beta * u;
+        tn = fma(C.beta, u, C.alpha * xt_t);
         if (J) {
           const double e1 = xq_t - yq, e2 = xv_t - yv, e3 = xt_t - yt;
-          c += 0.5 * C.w_y * (K.wy2q * e1 * e1 + K.wy2v * e2 * e2 + K.wy2t * e3 * e3);
-          c += 0.5 * C.w_w * u * u;
+          c = fma(0.5 * C.w_y, fma(K.wy2t * e3, e3, fma(K.wy2v * e2, e2, (K.wy2q * e1) * e1)), c);
+          c = fma(0.5 * C.w_w, u * u, c);
           const double ov = fabs(u) - K.wslim;
           const double oo = ov > 0.0 ? ov : 0.0;
-          c += C.w_ws * (0.5 * oo * oo);
+          c = fma(C.w_ws, 0.5 * (oo * oo), c);
         }
       }
       cost += g8_sum(c);
-      const int xbad = g8_or((J && (bad(fabs(qn)) || bad(fabs(vn)) || (FF && bad(fabs(tn))))) ? 1 : 0);
-      if (bad(cost) || xbad) {
+      int brk = (bad(cost) || g8_or((J && (bad(fabs(qn)) || bad(fabs(vn)) || (FF && bad(fabs(tn))))) ? 1 : 0)) ? 1 : 0;
+      if (ROW) brk = ls_row_bcast0(brk);  // the phantom group follows the real one
+      if (brk) {
         fail = true;
         break;
       }
@@ -1860,15 +1883,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
       double qn, vn, cp, lam[3];
       const int mode = FF ? MODE_TERMINAL_U : MODE_TERMINAL_X;
       PP(8);
-      node_calc_g8<NC>(C, K, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam
+      ls_node_calc<NC, ROW>(C, K, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam
 #ifdef FFDDP_PHASE_PROF
-                       , pp_acc, pp_last
+                            , pp_acc, pp_last
 #endif
       );
       double c = FF ? C.dt * cp : cp;
       if (FF && J) {
         const double e1 = xq_t - yq, e2 = xv_t - yv, e3 = xt_t - yt;
-        c += 0.5 * C.w_y * (K.wy2q * e1 * e1 + K.wy2v * e2 * e2 + K.wy2t * e3 * e3);
+        c = fma(0.5 * C.w_y, fma(K.wy2t * e3, e3, fma(K.wy2v * e2, e2, (K.wy2q * e1) * e1)), c);
       }
       cost += g8_sum(c);
       if (bad(cost)) fail = true;
@@ -1877,12 +1900,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
   PP(9);
   PP_FLUSH_AT(16);
   const double dv = g8_sum(dvp);
-  if (li == 0) {
+  if (li == 0 && real) {
     d.trial[((long)b * NTRIALS + tr) * 2 + 0] = cost;
     d.trial[((long)b * NTRIALS + tr) * 2 + 1] = dv;
     d.trial_fail[(long)b * NTRIALS + tr] = fail ? 1 : 0;
   }
 }
+#pragma clang fp contract(fast)
 
 // ---------------------------------------------------------------------------
 // acceptance / regularisation / stopping: one lane per instance
@@ -2288,6 +2312,9 @@ struct ffddp_handle {
   bool fw_fill = true;   // widen the first line-search pass to fill the SIMDs (FFDDP_FW_FILL=0: off)
   int fw_wide_max = -1;  // active instances per slice up to which the first pass takes every step length
                          // (decided on the device; FFDDP_FW_WIDE_MAX; -1: SIMDs / slices; 0: never)
+  int ls_row_max = -1;   // trial groups of a line-search pass up to which it runs one group per DPP row
+                         // (decided on the device; FFDDP_LS_ROW_MAX; -1: 4 SIMDs / slices, one wave
+                         // per SIMD share; 0: never)
   // optional per-kernel timing
   bool prof = false;
   int prof_mask = 0;
@@ -2532,11 +2559,25 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
         // iteration)
         const int wide = h->fw_wide_max >= 0 ? h->fw_wide_max : h->n_simd / S;
         const long g1 = std::max((long)Bk * n1, (long)std::min(Bk, wide) * NTRIALS);  // first-pass groups
+        // layout of each pass (ffddp_rollout.hpp): one trial group per DPP
+        // row while the pass's groups fit row_max, two otherwise, decided on
+        // the device from the active count; when every possible pass of this
+        // slice fits, only the row layout is launched
+        const int row_max = h->ls_row_max >= 0 ? h->ls_row_max : 4 * h->n_simd / S;
+        const bool row_only = (long)Bk * NTRIALS <= (long)row_max;
         auto fw = [&](int tr0, int ntr, int more) {
           const long groups = more ? (long)Bk * ntr : g1;
-          const dim3 grid((unsigned)((groups * G8 + 63) / 64));
-          hipLaunchKernelGGL((k_forward_g8<NC, FF>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk, surfk, tr0,
-                             ntr, more, it & 1, wide);
+          if (!row_only) {
+            const dim3 grid((unsigned)((groups * G8 + 63) / 64));
+            hipLaunchKernelGGL((k_forward_g8<NC, FF, false>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
+                               surfk, tr0, ntr, more, it & 1, wide, row_max);
+          }
+          if (row_max > 0) {
+            const long rg = std::min(groups, (long)row_max);  // the row layout runs only when they fit
+            const dim3 grid((unsigned)((rg * 16 + 63) / 64));
+            hipLaunchKernelGGL((k_forward_g8<NC, FF, true>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
+                               surfk, tr0, ntr, more, it & 1, wide, row_max);
+          }
         };
         {
           ProfScope p(h, ss, KC_FORWARD);
@@ -2739,6 +2780,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     if (const char* bw2 = std::getenv("FFDDP_BW_W2_MAX")) h->bw_w2_max = std::atoi(bw2);
     if (const char* ff = std::getenv("FFDDP_FW_FILL")) h->fw_fill = std::atoi(ff) != 0;
     if (const char* fwm = std::getenv("FFDDP_FW_WIDE_MAX")) h->fw_wide_max = std::atoi(fwm);
+    if (const char* lrm = std::getenv("FFDDP_LS_ROW_MAX")) h->ls_row_max = std::atoi(lrm);
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
       h->fw_sched.clear();
       for (const char* p = fsch; *p;) {

@@ -171,9 +171,15 @@ def test_c5_whole_workload_point3d_n100_b8192(monkeypatch):
         idx = picks[i0:i0 + 8]
         small.solve(_sub(batch, idx), maxiter=10)
         for j, i in enumerate(idx):
-            for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred", "stats"):
+            for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred"):
                 a, b = getattr(big, name)[i], getattr(small, name)[j]
                 assert np.array_equal(a, b, equal_nan=True), (name, int(i))
+            # solver counters equal; the line-search launch counters (stats
+            # 5..7: launches, step lengths evaluated per pass) follow the
+            # first pass's width, which the launch schedule sets from the
+            # batch size (8 instances: all ten step lengths at once)
+            keep = [c for c in range(big.stats.shape[1]) if c not in (5, 6, 7)]
+            assert np.array_equal(big.stats[i, keep], small.stats[j, keep]), ("stats", int(i))
     sel = picks[::3]
     from oracle import fddp
 

@@ -401,6 +401,11 @@ ENV_VARIANTS = [
     # instances, all ten step lengths in one pass below
     {"FFDDP_FW_FILL": "0", "FFDDP_FW_WIDE_MAX": "60"}, {"FFDDP_FW_FILL": "0"},
     {"FFDDP_BW_W2_MAX": "0"}, {"FFDDP_BW_W2_MAX": "100000"},
+    # line-search lane layout (ffddp_rollout.hpp): never / always one trial
+    # group per DPP row, and the device-side switch at a threshold the
+    # batch crosses between iterations
+    {"FFDDP_LS_ROW_MAX": "0"}, {"FFDDP_LS_ROW_MAX": "100000"}, {"FFDDP_LS_ROW_MAX": "90"},
+    {"FFDDP_LS_ROW_MAX": "90", "FFDDP_FW_FILL": "0", "FFDDP_FW_WIDE_MAX": "0"},
 ]
 
 

@@ -5,6 +5,7 @@
 #   fp64    fp64 PMC pass per kernel class, classical B=4096 and FF B=4096 (tools/pmc_fp64.sh)
 #   bits    in-tree library vs lib/base bit for bit (tools/lib_dump.py)
 #   nccl    one-process RCCL group: bench at B=4096 / 512 with --gather none / costs / full
+#   queue   RCCL communicator vs the slice streams' hardware queues (tools/nccl_queue.py)
 #   tests   pytest -m gpu with the parity log
 #   bench   one default bench line
 #   quick   short bench lines at B = 4096 / 1024 / 512 (no extras)
@@ -28,6 +29,11 @@ for st in $STEPS; do
               --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/nccl_${B}_$g.log 2>&1 || { tail -20 $O/nccl_${B}_$g.log; exit 1; }
             python3 -c "import json; d=json.loads(open('$O/nccl_${B}_$g.log').read().strip().splitlines()[-1]); print($B, '$g', round(d['value']), 'ms/step %.3f' % d['ms_per_step'])" | tee -a $O/nccl.txt
           done; done ;;
+    queue) for B in 4096 512; do for m in none rccl_first solver_first; do for g in none full; do
+            [ $m = none ] && [ $g = full ] && continue
+            timeout -k 10 120 python3 tools/nccl_queue.py --mode $m --batch $B --gather $g > $O/q_${m}_${B}_$g.log 2>&1 || { tail -20 $O/q_${m}_${B}_$g.log; exit 1; }
+            tail -1 $O/q_${m}_${B}_$g.log | tee -a $O/queue.txt
+          done; done; done ;;
     tests) rm -f $O/parity.jsonl
         FFDDP_PARITY_LOG=$O/parity.jsonl timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
           --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
