@@ -8,6 +8,8 @@
 #   queue   RCCL communicator vs the slice streams' hardware queues (tools/nccl_queue.py)
 #   tests   pytest -m gpu with the parity log
 #   bench   one default bench line
+#   ab      lib/base vs the in-tree library, then line-search layout thresholds (FFDDP_LS_ROW_MAX)
+#   forced  bench with a forced one-process RCCL group vs without (gather none)
 #   quick   short bench lines at B = 4096 / 1024 / 512 (no extras)
 # usage: [STEPS="tests bench"] tools/gpu_r05.sh TAG
 set -e
@@ -40,6 +42,16 @@ for st in $STEPS; do
         tail -1 $O/gpu_tests.log ;;
     bench) timeout -k 10 400 python3 bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
         tail -1 $O/bench.log | cut -c1-300 ;;
+    ab) STEPS=10 BATCHES="4096 1024 512" bash tools/ab_libs.sh $TAG/ab base main
+        STEPS=10 BATCHES="4096 1024 512" bash tools/ab_env.sh $TAG/abe "FFDDP_LS_ROW_MAX=0" "-" "FFDDP_LS_ROW_MAX=128" "FFDDP_LS_ROW_MAX=1024" ;;
+    forced) for B in 4096 512; do
+          timeout -k 10 200 python3 bench.py --batch $B --force-collective --gather none --steps 20 --warmup 3 \
+            --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/forced_$B.log 2>&1 || { tail -20 $O/forced_$B.log; exit 1; }
+          python3 -c "import json; d=json.loads(open('$O/forced_$B.log').read().strip().splitlines()[-1]); print('forced', $B, round(d['value']))"
+          timeout -k 10 200 python3 bench.py --batch $B --gather none --steps 20 --warmup 3 \
+            --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/plain_$B.log 2>&1 || { tail -20 $O/plain_$B.log; exit 1; }
+          python3 -c "import json; d=json.loads(open('$O/plain_$B.log').read().strip().splitlines()[-1]); print('plain', $B, round(d['value']))"
+        done ;;
     quick) for B in 4096 1024 512; do
         timeout -k 10 200 python3 bench.py --batch $B --no-cpu-baseline --no-extras --no-host-io > $O/q_$B.log 2>&1 || { tail -20 $O/q_$B.log; exit 1; }
         python3 -c "import json; d=json.loads(open('$O/q_$B.log').read().strip().splitlines()[-1]); k=d['kernels']; print($B, round(d['value']), 'ms/step %.2f'%d['ms_per_step'], ' '.join('%s=%.0f'%(n,v['avg_launch_ms']*1e3) for n,v in k.items()))"

@@ -32,11 +32,11 @@ int main() {
   hipEvent_t a, z;
   hipEventCreate(&a);
   hipEventCreate(&z);
-  constexpr int ITER = 4096;
+  constexpr int ITER = 32768;
   std::printf("device %s, %d CUs, clock %d kHz\n", p.name, cus, p.clockRate);
   std::printf("%-10s %-10s %12s %14s %16s\n", "waves/SIMD", "blocks", "ms", "TFLOP/s", "instr/SIMD/clk");
   double best = 0.0;
-  for (int wps : {1, 2, 4, 8}) {
+  for (int wps : {1, 2, 4, 8, 16}) {
     const int blocks = cus * wps;  // 256 threads = 4 waves per block: one per SIMD
     for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k_fma<ITER>, dim3(blocks), dim3(256), 0, 0, sink, 1.0000001, 1e-9);
     hipDeviceSynchronize();
