@@ -519,7 +519,7 @@ template <bool FF> struct BwW {
   static constexpr int REC = rec_words(NX);
   double R[(REC + 63) / 64 * 64];  // staged node record (A | Lxx | Lxu | Luu | Lx | Lu | cost | lam), padded
   double V[NX * NX];  // V_xx' on entry to a node, V_xx on exit
-  double Q[ND * ND + 1];  // [[Qxx, Qxu], [Qux, Quu + preg I]]; Q[ND * ND]: phase C's spare lanes store here
+  double Q[ND * ND];  // [[Qxx, Qxu], [Qux, Quu + preg I]]
   double W[NX * NU];  // V D
   double Y[NU * NU];  // D' V D
   double M[ND * NU];
@@ -534,6 +534,10 @@ template <bool FF> struct BwW {
   int flag;
   int badw[2];  // k_backward_w2: per-wave NaN flags of phases F / G
   int clamped[NU];
+  // phase C's spare lanes store here (the last member: a slot inside the
+  // struct would shift the arrays after it, i.e. their LDS bank mapping;
+  // measured: backward 350 -> 536 us per launch at B = 4096)
+  double qspare;
 };
 
 // nonzeros of column c of I~ (the Euler identity part of [Fx Fu]):
@@ -797,7 +801,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 #pragma unroll
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
-    const bool spare = l + 64 * k >= NQE;  // past the last entry: computes entry (0, 0), stores to Q[ND * ND]
+    const bool spare = l + 64 * k >= NQE;  // past the last entry: computes entry (0, 0), stores to S.qspare
     if (!spare) tri_rc(l + 64 * k, r, c);
     qrc[k] = (spare ? 1 << 16 : 0) | (r << 8) | c;
   }
@@ -922,7 +926,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 #pragma unroll QC_N
       for (int k = 0; k < NQL; ++k) {
         // no range guard: a lane past the last entry computes entry (0, 0)
-        // (qrc's default) and stores it to the spare slot Q[ND * ND] (the
+        // (qrc's default) and stores it to the spare slot S.qspare (the
         // address is selected, not the branch), so the passes need no
         // divergent branch and can interleave, and no entry has two writers
         {
@@ -951,8 +955,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-          S.Q[spare ? ND * ND : r * ND + c] = v;
-          S.Q[spare ? ND * ND : c * ND + r] = v;
+          *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
+          *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
@@ -1192,7 +1196,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
-    const bool spare = tid + 128 * k >= NQE;  // past the last entry: computes entry (0, 0), stores to Q[ND * ND]
+    const bool spare = tid + 128 * k >= NQE;  // past the last entry: computes entry (0, 0), stores to S.qspare
     if (!spare) tri_rc(tid + 128 * k, r, c);
     qrc[k] = (spare ? 1 << 16 : 0) | (r << 8) | c;
   }
@@ -1384,7 +1388,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
       for (int k = 0; k < NQL; ++k) {
         // no range guard: a lane past the last entry computes entry (0, 0)
-        // (qrc's default) and stores it to the spare slot Q[ND * ND] (the
+        // (qrc's default) and stores it to the spare slot S.qspare (the
         // address is selected, not the branch), so the passes need no
         // divergent branch and can interleave, and no entry has two writers
         {
@@ -1413,8 +1417,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-          S.Q[spare ? ND * ND : r * ND + c] = v;
-          S.Q[spare ? ND * ND : c * ND + r] = v;
+          *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
+          *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
@@ -2561,10 +2565,15 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
         const long g1 = std::max((long)Bk * n1, (long)std::min(Bk, wide) * NTRIALS);  // first-pass groups
         // layout of each pass (ffddp_rollout.hpp): one trial group per DPP
         // row while the pass's groups fit row_max, two otherwise, decided on
-        // the device from the active count; when every possible pass of this
-        // slice fits, only the row layout is launched
-        const int row_max = h->ls_row_max >= 0 ? h->ls_row_max : 4 * h->n_simd / S;
-        const bool row_only = (long)Bk * NTRIALS <= (long)row_max;
+        // the device from the active count.  Only slices that fit one wave
+        // per SIMD share take the row layout at all: a large slice's late
+        // passes would gain it, but launching both layouts every pass (the
+        // unchosen one exits at once) cost more than that at B = 4096
+        // (507.9k vs 512.4k solves/s).  When every possible
+        // pass of the slice fits, only the row layout is launched.
+        const int row_max = (h->ls_row_max >= 0 ? h->ls_row_max : 4 * h->n_simd / S) *
+                            (h->ls_row_max < 0 && Bk > h->n_simd / S ? 0 : 1);
+        const bool row_only = row_max > 0 && (long)Bk * NTRIALS <= (long)row_max;
         auto fw = [&](int tr0, int ntr, int more) {
           const long groups = more ? (long)Bk * ntr : g1;
           if (!row_only) {

@@ -90,8 +90,9 @@ class BatchedBoxFDDP:
         """crocoddyl solver.setCallbacks (crocoddyl_classical.py:353): the device
         keeps a per-iteration record (include/ffddp.h ffddp_trace_*); every
         callback is called with (solver, trace) after each solve."""
-        self._callbacks = list(callbacks)
-        self.trace_enable(max_iters if self._callbacks else 0)
+        callbacks = list(callbacks)
+        self.trace_enable(max_iters if callbacks else 0)  # raises while a SolvePlan is open
+        self._callbacks = callbacks
 
     def getCallbacks(self):
         return list(self._callbacks)

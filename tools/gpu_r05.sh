@@ -10,6 +10,7 @@
 #   bench   one default bench line
 #   ab      lib/base vs the in-tree library, then line-search layout thresholds (FFDDP_LS_ROW_MAX)
 #   forced  bench with a forced one-process RCCL group vs without (gather none)
+#   small   configs[4] per-GPU shape (N=100 point3d B=1024) and the C1 tick breakdown, lib/base vs in-tree
 #   quick   short bench lines at B = 4096 / 1024 / 512 (no extras)
 # usage: [STEPS="tests bench"] tools/gpu_r05.sh TAG
 set -e
@@ -31,7 +32,7 @@ for st in $STEPS; do
               --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/nccl_${B}_$g.log 2>&1 || { tail -20 $O/nccl_${B}_$g.log; exit 1; }
             python3 -c "import json; d=json.loads(open('$O/nccl_${B}_$g.log').read().strip().splitlines()[-1]); print($B, '$g', round(d['value']), 'ms/step %.3f' % d['ms_per_step'])" | tee -a $O/nccl.txt
           done; done ;;
-    queue) for B in 4096 512; do for m in none rccl_first solver_first; do for g in none full; do
+    queue) for B in 4096 512; do for m in none rccl_first solver_first bench_order; do for g in none full; do
             [ $m = none ] && [ $g = full ] && continue
             timeout -k 10 120 python3 tools/nccl_queue.py --mode $m --batch $B --gather $g > $O/q_${m}_${B}_$g.log 2>&1 || { tail -20 $O/q_${m}_${B}_$g.log; exit 1; }
             tail -1 $O/q_${m}_${B}_$g.log | tee -a $O/queue.txt
@@ -51,6 +52,13 @@ for st in $STEPS; do
           timeout -k 10 200 python3 bench.py --batch $B --gather none --steps 20 --warmup 3 \
             --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/plain_$B.log 2>&1 || { tail -20 $O/plain_$B.log; exit 1; }
           python3 -c "import json; d=json.loads(open('$O/plain_$B.log').read().strip().splitlines()[-1]); print('plain', $B, round(d['value']))"
+        done ;;
+    small) for L in base main; do
+          if [ $L = main ]; then LIB=$R/franka-force-feedback-mpc_amd/lib/libffddp.so; else LIB=$R/franka-force-feedback-mpc_amd/lib/$L/libffddp.so; fi
+          FFDDP_LIB=$LIB timeout -k 10 200 python3 bench.py --horizon 100 --contact point3d --batch 1024 --no-extras --no-cpu-baseline --no-host-io > $O/c5_$L.log 2>&1 || { tail -20 $O/c5_$L.log; exit 1; }
+          python3 -c "import json; d=json.loads(open('$O/c5_$L.log').read().strip().splitlines()[-1]); k=d['kernels']; print('c5', '$L', round(d['value']), ' '.join('%s=%.0f'%(n,v['avg_launch_ms']*1e3) for n,v in k.items()))"
+          FFDDP_LIB=$LIB timeout -k 10 200 python3 tools/c1_breakdown.py --time 4 > $O/c1_$L.log 2>&1 || { tail -20 $O/c1_$L.log; exit 1; }
+          echo "c1 $L $(tail -1 $O/c1_$L.log | cut -c1-400)"
         done ;;
     quick) for B in 4096 1024 512; do
         timeout -k 10 200 python3 bench.py --batch $B --no-cpu-baseline --no-extras --no-host-io > $O/q_$B.log 2>&1 || { tail -20 $O/q_$B.log; exit 1; }

@@ -21,7 +21,7 @@ import ffddp_path  # noqa: E402,F401
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=("none", "rccl_first", "solver_first"), required=True)
+    ap.add_argument("--mode", choices=("none", "rccl_first", "solver_first", "bench_order"), required=True)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--gather", choices=("none", "costs", "full"), default="none")
     ap.add_argument("--steps", type=int, default=20)
@@ -32,6 +32,11 @@ def main():
     from ffddp import BatchedBoxFDDP, _abi, robot as R, shard, workload
     from ffddp.config import classical_preset
 
+    import os
+    aff0 = len(os.sched_getaffinity(0))
+    if a.mode == "bench_order":  # bench.py's order: the process group before anything else
+        shard.init("nccl", 0, 1, force=True)
+    aff1 = len(os.sched_getaffinity(0))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     B, N = a.batch, 30
@@ -53,8 +58,9 @@ def main():
         solver = BatchedBoxFDDP(cfg, max_batch=B, device=0)
         solver.solve_dev(T, stream=stream)
         torch.cuda.synchronize(dev)
-    if a.mode != "none":
+    if a.mode in ("rccl_first", "solver_first"):
         shard.init("nccl", 0, 1, force=True)
+    aff2 = len(os.sched_getaffinity(0))
     if solver is None:
         solver = BatchedBoxFDDP(cfg, max_batch=B, device=0)
     gather = None
@@ -70,12 +76,16 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    enq = 0.0
     for _ in range(a.steps):
+        te = time.perf_counter()
         step()
+        enq += time.perf_counter() - te
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     print(json.dumps({"mode": a.mode, "batch": B, "gather": a.gather, "value": B * a.steps / el,
-                      "ms_per_step": el / a.steps * 1e3}))
+                      "ms_per_step": el / a.steps * 1e3, "host_enqueue_ms_per_step": enq / a.steps * 1e3,
+                      "affinity_cpus": [aff0, aff1, aff2]}))
     if dist.is_initialized():
         dist.destroy_process_group()
 
