@@ -1840,9 +1840,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
       {
         double acc = fma(-pk, alpha, pus);
         const double dq = xq_t - sq, dv = xv_t - sv, dtt = xt_t - stt;
-#if FFDDP_FUSED_BC
-        acc = FF ? dbc_ctrl3<ROW>(acc, dq, dv, dtt, pK) : dbc_ctrl2<ROW>(acc, dq, dv, pK);
-#else
 #pragma unroll
         for (int m = 0; m < NQ; ++m) {
           const double dqm = ls_get<ROW>(dq, m), dvm = ls_get<ROW>(dv, m);
@@ -1850,7 +1847,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
           acc = fma(-pK[7 + m], dvm, acc);
           if (FF) acc = fma(-pK[14 + m], ls_get<ROW>(dtt, m), acc);
         }
-#endif
         if (C.use_box) acc = fmin(fmax(acc, K.ulb), K.uub);
         u = acc;
         if (Js) utr[(long)t * NU + ji] = u;

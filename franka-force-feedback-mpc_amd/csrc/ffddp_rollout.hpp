@@ -23,16 +23,7 @@
 // node_primal (ffddp_node.hpp); only the evaluation order differs.
 #pragma once
 
-#include "ffddp_dppfma.hpp"
 #include "ffddp_group.hpp"
-
-// FFDDP_FUSED_BC: broadcast-fed FMAs as one v_fmac_f64_dpp row_newbcast per
-// term (two bank-masked ones in the shared layout) instead of a broadcast
-// move and an FMA (ffddp_dppfma.hpp, generated by tools/gen_dppfma.py).
-// Same single rounding per term, so the same bits either way.
-#ifndef FFDDP_FUSED_BC
-#define FFDDP_FUSED_BC 1
-#endif
 
 #pragma clang fp contract(off)
 
@@ -131,47 +122,6 @@ __device__ __forceinline__ double ls_friction_cone(const DevConsts& C, const dou
 
 // ---- group primitives per layout ----
 template <bool ROW> __device__ __forceinline__ double ls_get(double v, int src) { return g8_get<ROW>(v, src); }
-#if FFDDP_FUSED_BC
-// lane-index dispatch of the fused blocks (k is a constant after unrolling)
-template <bool ROW>
-__device__ __forceinline__ double ls_dot6_bc(int k, double a0, double a1, double a2, double a3, double a4, double a5,
-                                             double b0, double b1, double b2, double b3, double b4, double b5) {
-#define FFDDP_D6(K) return dbc_dot6<ROW, K>(0.0, a0, a1, a2, a3, a4, a5, b0, b1, b2, b3, b4, b5)
-  switch (k) {
-    case 0: FFDDP_D6(0);
-    case 1: FFDDP_D6(1);
-    case 2: FFDDP_D6(2);
-    case 3: FFDDP_D6(3);
-    case 4: FFDDP_D6(4);
-    case 5: FFDDP_D6(5);
-    default: FFDDP_D6(6);
-  }
-#undef FFDDP_D6
-}
-template <bool ROW> __device__ __forceinline__ double ls_chol_bc(int k, double acc, const double (&a)[NQ]) {
-  switch (k) {
-    case 1: return dbc_chol<ROW, 1>(acc, a);
-    case 2: return dbc_chol<ROW, 2>(acc, a);
-    case 3: return dbc_chol<ROW, 3>(acc, a);
-    case 4: return dbc_chol<ROW, 4>(acc, a);
-    case 5: return dbc_chol<ROW, 5>(acc, a);
-    case 6: return dbc_chol<ROW, 6>(acc, a);
-    default: return acc;
-  }
-}
-template <bool ROW> __device__ __forceinline__ double ls_bwd_bc(int k, double acc, double l, const double (&x)[NQ]) {
-  switch (k) {
-    case 0: return dbc_bwd<ROW, 0>(acc, l, x);
-    case 1: return dbc_bwd<ROW, 1>(acc, l, x);
-    case 2: return dbc_bwd<ROW, 2>(acc, l, x);
-    case 3: return dbc_bwd<ROW, 3>(acc, l, x);
-    case 4: return dbc_bwd<ROW, 4>(acc, l, x);
-    case 5: return dbc_bwd<ROW, 5>(acc, l, x);
-    default: return acc;
-  }
-}
-#endif
-
 // prefix-scan step over n values: x += x[li - d] (lanes li < d keep x).
 // SHARED: one exec-masked block (three scalar instructions for the block,
 // not a select per value).  ROW: unmasked (a source outside the row reads 0).
@@ -204,13 +154,9 @@ template <bool ROW> __device__ __forceinline__ void ls_chol_rows(double (&a)[NQ]
 #pragma unroll
     for (int m = 0; m < k; ++m) d = fma(-a[m], a[m], d);
     const double il = ls_rsqrt(ls_get<ROW>(d, k));
-#if FFDDP_FUSED_BC
-    const double s = ls_chol_bc<ROW>(k, a[k], a);
-#else
     double s = a[k];
 #pragma unroll
     for (int m = 0; m < k; ++m) s = fma(-a[m], ls_get<ROW>(a[m], k), s);
-#endif
     a[k] = (li == k) ? il : ((li > k) ? s * il : a[k]);
   }
 }
@@ -224,19 +170,15 @@ template <bool ROW> __device__ __forceinline__ void ls_fwd(const double (&Lr)[NQ
     y[k] = ls_get<ROW>(s * Lr[k], k);
   }
 }
-// L^T x = y (y group-uniform; L held as rows, Lr[k] of lane m = L_mk): this lane's x
-template <bool ROW> __device__ __forceinline__ double ls_bwd(const double (&Lr)[NQ], const double (&y)[NQ], int li) {
+// L^T x = y (y group-uniform): this lane's x
+template <bool ROW> __device__ __forceinline__ double ls_bwd(const double (&Lt)[NQ][NQ], const double (&y)[NQ], int li) {
   double x[NQ];
 #pragma unroll
   for (int k = NQ - 1; k >= 0; --k) {
-#if FFDDP_FUSED_BC
-    const double s = ls_bwd_bc<ROW>(k, y[k], Lr[k], x);
-#else
     double s = y[k];
 #pragma unroll
-    for (int m = k + 1; m < NQ; ++m) s = fma(-ls_get<ROW>(Lr[k], m), x[m], s);
-#endif
-    x[k] = s * ls_get<ROW>(Lr[k], k);
+    for (int m = k + 1; m < NQ; ++m) s = fma(-Lt[k][m], x[m], s);
+    x[k] = s * Lt[k][k];
   }
   double out = 0.0;
 #pragma unroll
@@ -507,13 +449,9 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K,
     double Lr[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-#if FFDDP_FUSED_BC
-      const double mkj = ls_dot6_bc<ROW>(k, Sv[0], Sv[1], Sv[2], z[0], z[1], z[2], Fl[0], Fl[1], Fl[2], Fa[0], Fa[1], Fa[2]);
-#else
       const double sx = ls_get<ROW>(Sv[0], k), sy = ls_get<ROW>(Sv[1], k), sz = ls_get<ROW>(Sv[2], k);
       const double zx = ls_get<ROW>(z[0], k), zy = ls_get<ROW>(z[1], k), zz = ls_get<ROW>(z[2], k);
       const double mkj = fma(zz, Fa[2], fma(zy, Fa[1], fma(zx, Fa[0], ls_dot3(sx, Fl[0], sy, Fl[1], sz, Fl[2]))));
-#endif
       Lr[k] = (k <= li) ? mkj : (li == k ? 1.0 : 0.0);
     }
     if (!J) {
@@ -522,6 +460,12 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K,
     }
     PP(4);
     ls_chol_rows<ROW>(Lr, li);
+    // L^T by rows, group-uniform: Lt[k][m] = L[m][k] (m >= k) from lane m
+    double Lt[NQ][NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+#pragma unroll
+      for (int m = k; m < NQ; ++m) Lt[k][m] = ls_get<ROW>(Lr[k], m);
     double y1[NQ];
     ls_fwd<ROW>(Lr, u - tau, y1);
     PP(5);
@@ -594,11 +538,11 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K,
         for (int r = 0; r < NC; ++r) s = fma(-Y[r][k], yl[r], s);
         y2[k] = s;
       }
-      a = ls_bwd<ROW>(Lr, y2, li);
+      a = ls_bwd<ROW>(Lt, y2, li);
 #pragma unroll
       for (int r = 0; r < NC; ++r) lam[r] = -yl[r];
     } else {
-      a = ls_bwd<ROW>(Lr, y1, li);
+      a = ls_bwd<ROW>(Lt, y1, li);
     }
   }
   PP(6);

@@ -43,8 +43,8 @@ for st in $STEPS; do
         tail -1 $O/gpu_tests.log ;;
     bench) timeout -k 10 400 python3 bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
         tail -1 $O/bench.log | cut -c1-300 ;;
-    ab) STEPS=10 BATCHES="4096 1024 512" bash tools/ab_libs.sh $TAG/ab base unfused main ;;
-    abrow) STEPS=10 BATCHES="4096 1024 512" bash tools/ab_env.sh $TAG/abe "FFDDP_LS_ROW_MAX=0" "-" "FFDDP_LS_ROW_MAX=128" "FFDDP_LS_ROW_MAX=1024" ;;
+    ab) STEPS=10 BATCHES="4096 1024 512" bash tools/ab_libs.sh $TAG/ab base main
+        STEPS=10 BATCHES="4096 1024 512" bash tools/ab_env.sh $TAG/abe "FFDDP_LS_ROW_MAX=0" "-" "FFDDP_LS_ROW_MAX=128" "FFDDP_LS_ROW_MAX=1024" ;;
     forced) for B in 4096 512; do
           timeout -k 10 200 python3 bench.py --batch $B --force-collective --gather none --steps 20 --warmup 3 \
             --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/forced_$B.log 2>&1 || { tail -20 $O/forced_$B.log; exit 1; }
@@ -53,7 +53,7 @@ for st in $STEPS; do
             --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/plain_$B.log 2>&1 || { tail -20 $O/plain_$B.log; exit 1; }
           python3 -c "import json; d=json.loads(open('$O/plain_$B.log').read().strip().splitlines()[-1]); print('plain', $B, round(d['value']))"
         done ;;
-    small) for L in base unfused main; do
+    small) for L in base main; do
           if [ $L = main ]; then LIB=$R/franka-force-feedback-mpc_amd/lib/libffddp.so; else LIB=$R/franka-force-feedback-mpc_amd/lib/$L/libffddp.so; fi
           FFDDP_LIB=$LIB timeout -k 10 200 python3 bench.py --horizon 100 --contact point3d --batch 1024 --no-extras --no-cpu-baseline --no-host-io > $O/c5_$L.log 2>&1 || { tail -20 $O/c5_$L.log; exit 1; }
           python3 -c "import json; d=json.loads(open('$O/c5_$L.log').read().strip().splitlines()[-1]); k=d['kernels']; print('c5', '$L', round(d['value']), ' '.join('%s=%.0f'%(n,v['avg_launch_ms']*1e3) for n,v in k.items()))"
