@@ -275,13 +275,18 @@ def main():
     # FFDDP_BENCH_ONE_GPU=1: every rank on cuda:0 with gloo collectives, a
     # one-GPU rehearsal of the N > 1 path (slices, max-over-ranks timing,
     # gather); never how the metric is measured
-    if os.environ.get("FFDDP_BENCH_ONE_GPU") == "1":
-        shard.init("gloo", local_rank, world)
+    one_gpu = os.environ.get("FFDDP_BENCH_ONE_GPU") == "1"
+    dev_rank = local_rank
+    if one_gpu:
         local_rank = 0
-    else:
-        shard.init("nccl", local_rank, world, force=args.force_collective)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
+    # The device, the null stream and the solver's slice streams come first,
+    # the process group after them: streams created after RCCL's own took
+    # shared hardware queues (4 per process) and the solve ran 34 % (B=4096)
+    # to 47 % (B=512) slower with an idle communicator in the process
+    # (tools/nccl_queue.py)
+    torch.zeros(1, device=dev)
 
     B, N, nu = args.batch, args.horizon, 7
     cfg = ff_preset(N, args.contact) if args.variant == "ff" else classical_preset(N, args.contact)
@@ -317,7 +322,11 @@ def main():
     mine = glob
     T = tensors(mine)
     counts = [B] * world
-    solver = BatchedBoxFDDP(cfg, max_batch=B, device=local_rank)
+    solver = BatchedBoxFDDP(cfg, max_batch=B, device=local_rank)  # creates the slice streams
+    if one_gpu:
+        shard.init("gloo", dev_rank, world)
+    else:
+        shard.init("nccl", local_rank, world, force=args.force_collective)
     gather = None
     if (world > 1 or args.force_collective) and args.gather != "none":
         width = shard.pack_results(T, args.gather).shape[1]

@@ -58,6 +58,11 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 #ifndef QC_UNROLL
 #define QC_UNROLL 1
 #endif
+// FFDDP_QSPARE: phase C's spare lanes (past the last Q entry) store to a
+// slot of their own (1), or rewrite entry (0, 0) with its owner's bits (0)
+#ifndef FFDDP_QSPARE
+#define FFDDP_QSPARE 1
+#endif
 #ifndef BW_WAVES
 #define BW_WAVES 1
 #endif
@@ -955,8 +960,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
+#if FFDDP_QSPARE
           *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
           *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
+#else
+          (void)spare;
+          S.Q[r * ND + c] = v;
+          S.Q[c * ND + r] = v;
+#endif
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
@@ -1417,8 +1428,14 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
+#if FFDDP_QSPARE
           *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
           *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
+#else
+          (void)spare;
+          S.Q[r * ND + c] = v;
+          S.Q[c * ND + r] = v;
+#endif
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
@@ -2806,6 +2823,14 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
       const int v = std::atoi(f1);
       h->fw_first = v < 1 ? 1 : (v > NTRIALS ? NTRIALS : v);
     }
+  }
+  // the slice streams now, not at the first solve: a process's first
+  // streams get hardware queues of their own (GPU_MAX_HW_QUEUES, 4), and a
+  // communicator created before them (RCCL's streams) would leave the
+  // slices sharing queues
+  if (h->nstreams > 1 && !stream_pool_acquire(h->device, h->nstreams, h->streams)) {
+    delete h;
+    return FFDDP_E_DEVICE;
   }
   int rc = 0;
   rc |= dalloc(h, &h->dc, 1);

@@ -275,30 +275,46 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
       for (int k = 0; k < NQ; ++k)
         if (k <= li) gp->L[tri(li, k)] = Lr[k];
     }
-    const double af = g8_solve<true>(Lr, u - tau, li);
+    // y1 = L^-1 (u - tau); free: a = L^-T y1.  Contact (the KKT by its Schur
+    // complement): Y = L^-1 Jc^T, S = Y'Y + eps, yl = S^-1 (gamma + Y'y1),
+    // a = L^-T (y1 - Y yl), lambda = -yl: one backward substitution, and the
+    // Schur sums from the group-uniform forward solutions (no cross-lane sums)
+    double y1[NQ];
+    g8_fwd_all<true>(Lr, u - tau, y1);
     if (surface) {
       constexpr int c0 = NC == 1 ? 2 : 0;
       const double pstar[3] = {ref[0], ref[1], ref[2] - C.z_press};
       double rel[3] = {pee[0] - o[0], pee[1] - o[1], pee[2] - o[2]};
       double jcol[3];
       cross3(z, rel, jcol);
-      double Jc[3], Y[3], gam[3];
+      double Yu[3][NQ], gam[3];
 #pragma unroll
       for (int r = 0; r < NC; ++r) {
-        Jc[r] = J ? jcol[c0 + r] : 0.0;
+        const double Jc = J ? jcol[c0 + r] : 0.0;
         gam[r] = ap0[c0 + r] + C.Kp * (pee[c0 + r] - pstar[c0 + r]) + C.Kd * vp[c0 + r];
-        Y[r] = g8_fwd<true>(Lr, Jc[r], li);
+        g8_fwd_all<true>(Lr, Jc, Yu[r]);
+        double yown = 0.0;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) yown = (li == k) ? Yu[r][k] : yown;
         if (J) {
-          gp->Jc[r][li] = Jc[r];
-          gp->Y[r][li] = Y[r];
+          gp->Jc[r][li] = Jc;
+          gp->Y[r][li] = yown;
         }
       }
       double S[6], yl[3];
 #pragma unroll
       for (int r = 0; r < NC; ++r) {
 #pragma unroll
-        for (int s2 = 0; s2 <= r; ++s2) S[tri(r, s2)] = g8_sum(J ? Y[r] * Y[s2] : 0.0) + (r == s2 ? C.eps : 0.0);
-        yl[r] = gam[r] + g8_sum(J ? Jc[r] * af : 0.0);
+        for (int s2 = 0; s2 <= r; ++s2) {
+          double acc = Yu[r][0] * Yu[s2][0];
+#pragma unroll
+          for (int k = 1; k < NQ; ++k) acc += Yu[r][k] * Yu[s2][k];
+          S[tri(r, s2)] = acc + (r == s2 ? C.eps : 0.0);
+        }
+        double acc = Yu[r][0] * y1[0];
+#pragma unroll
+        for (int k = 1; k < NQ; ++k) acc += Yu[r][k] * y1[k];
+        yl[r] = gam[r] + acc;
       }
       chol_packed<NC>(S);
       if (li == 0) {
@@ -306,15 +322,15 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
         for (int e = 0; e < NC * (NC + 1) / 2; ++e) gp->Ls[e] = S[e];
       }
       chol_solve<NC>(S, yl);
-      double rhs = 0.0;
 #pragma unroll
-      for (int r = 0; r < NC; ++r) rhs += Jc[r] * (-yl[r]);
-      a = af + g8_solve<true>(Lr, rhs, li);
+      for (int k = 0; k < NQ; ++k) {
+#pragma unroll
+        for (int r = 0; r < NC; ++r) y1[k] -= Yu[r][k] * yl[r];
+      }
 #pragma unroll
       for (int r = 0; r < NC; ++r) lam[r] = -yl[r];
-    } else {
-      a = af;
     }
+    a = g8_bwd_all<true>(Lr, y1, li);
   }
   if (!J) a = 0.0;
   if (J) gp->a[li] = a;

@@ -32,7 +32,7 @@ for st in $STEPS; do
               --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/nccl_${B}_$g.log 2>&1 || { tail -20 $O/nccl_${B}_$g.log; exit 1; }
             python3 -c "import json; d=json.loads(open('$O/nccl_${B}_$g.log').read().strip().splitlines()[-1]); print($B, '$g', round(d['value']), 'ms/step %.3f' % d['ms_per_step'])" | tee -a $O/nccl.txt
           done; done ;;
-    queue) for B in 4096 512; do for m in none rccl_first solver_first bench_order; do for g in none full; do
+    queue) for B in 4096 512; do for m in ${QMODES:-none rccl_first solver_first bench_order}; do for g in ${QGATHER:-none full}; do
             [ $m = none ] && [ $g = full ] && continue
             timeout -k 10 120 python3 tools/nccl_queue.py --mode $m --batch $B --gather $g > $O/q_${m}_${B}_$g.log 2>&1 || { tail -20 $O/q_${m}_${B}_$g.log; exit 1; }
             tail -1 $O/q_${m}_${B}_$g.log | tee -a $O/queue.txt
@@ -43,8 +43,8 @@ for st in $STEPS; do
         tail -1 $O/gpu_tests.log ;;
     bench) timeout -k 10 400 python3 bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
         tail -1 $O/bench.log | cut -c1-300 ;;
-    ab) STEPS=10 BATCHES="4096 1024 512" bash tools/ab_libs.sh $TAG/ab base main
-        STEPS=10 BATCHES="4096 1024 512" bash tools/ab_env.sh $TAG/abe "FFDDP_LS_ROW_MAX=0" "-" "FFDDP_LS_ROW_MAX=128" "FFDDP_LS_ROW_MAX=1024" ;;
+    ab) STEPS=10 BATCHES="${ABB:-4096 1024 512}" bash tools/ab_libs.sh $TAG/ab ${LIBS:-base main} ;;
+    abrow) STEPS=10 BATCHES="4096 1024 512" bash tools/ab_env.sh $TAG/abe "FFDDP_LS_ROW_MAX=0" "-" "FFDDP_LS_ROW_MAX=128" "FFDDP_LS_ROW_MAX=1024" ;;
     forced) for B in 4096 512; do
           timeout -k 10 200 python3 bench.py --batch $B --force-collective --gather none --steps 20 --warmup 3 \
             --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/forced_$B.log 2>&1 || { tail -20 $O/forced_$B.log; exit 1; }

@@ -21,7 +21,8 @@ import ffddp_path  # noqa: E402,F401
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=("none", "rccl_first", "solver_first", "bench_order"), required=True)
+    ap.add_argument("--mode", choices=("none", "rccl_first", "solver_first", "bench_order", "bench_touch",
+                                       "bench_solver"), required=True)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--gather", choices=("none", "costs", "full"), default="none")
     ap.add_argument("--steps", type=int, default=20)
@@ -34,7 +35,16 @@ def main():
 
     import os
     aff0 = len(os.sched_getaffinity(0))
-    if a.mode == "bench_order":  # bench.py's order: the process group before anything else
+    # bench_order: the process group before anything else (bench.py up to
+    # round 5); bench_touch: one device tensor first (the null stream in
+    # use); bench_solver: the solver handle first (its slice streams)
+    if a.mode == "bench_touch":
+        torch.cuda.set_device(0)
+        torch.zeros(1, device="cuda:0")
+    if a.mode == "bench_solver":
+        cfg0 = classical_preset(30, "normal_1d")
+        solver0 = BatchedBoxFDDP(cfg0, max_batch=a.batch, device=0)
+    if a.mode in ("bench_order", "bench_touch", "bench_solver"):
         shard.init("nccl", 0, 1, force=True)
     aff1 = len(os.sched_getaffinity(0))
     dev = torch.device("cuda", 0)
@@ -61,6 +71,8 @@ def main():
     if a.mode in ("rccl_first", "solver_first"):
         shard.init("nccl", 0, 1, force=True)
     aff2 = len(os.sched_getaffinity(0))
+    if a.mode == "bench_solver":
+        solver = solver0
     if solver is None:
         solver = BatchedBoxFDDP(cfg, max_batch=B, device=0)
     gather = None
