@@ -2441,8 +2441,11 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
   const int N = h->hc.N, nx = h->hc.nx;
   int S = h->nstreams;
   if (B < 64 * S) S = 1;
-  if (S > 1 && (int)h->streams.size() < S) {
-    if (!stream_pool_acquire(h->device, S, h->streams)) return fail(h, FFDDP_E_DEVICE, "hipStreamCreate failed");
+  if (S > 1) {
+    // the streams normally come with the handle (ffddp_create); the fork /
+    // join and stagger events on first use
+    if ((int)h->streams.size() < S && !stream_pool_acquire(h->device, S, h->streams))
+      return fail(h, FFDDP_E_DEVICE, "hipStreamCreate failed");
     while ((int)h->sev.size() < S + 1) {
       hipEvent_t e;
       HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -2864,12 +2867,14 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
   rc |= dalloc(h, &h->out_stats, (size_t)B * FFDDP_NSTATS);
   rc |= dalloc(h, &h->out_ok, (size_t)B);
   if (rc) {
+    if (!h->streams.empty()) stream_pool_release(h->device, (int)h->streams.size());
     free_all(h);
     delete h;
     return FFDDP_E_OOM;
   }
   if (hipMemcpy(h->dc, &h->hc, sizeof(DevConsts), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->drb, robot, sizeof(ffddp_robot), hipMemcpyHostToDevice) != hipSuccess) {
+    if (!h->streams.empty()) stream_pool_release(h->device, (int)h->streams.size());
     free_all(h);
     delete h;
     return FFDDP_E_DEVICE;
