@@ -8,6 +8,14 @@
 // the evaluation order (hence rounding) differs.
 #pragma once
 
+// k_node's contact solve: one backward substitution through the Schur
+// complement (1) or the two-solve form (0, default: on configs[1]'s random-x0
+// spread the Schur form doubled the distance of `us` from an
+// extended-precision solve, 1.7e-7 -> 3.3e-7, tools/ext_budget.py)
+#ifndef FFDDP_KN_SCHUR
+#define FFDDP_KN_SCHUR 0
+#endif
+
 #include "ffddp_group.hpp"
 
 namespace ffddp {
@@ -275,6 +283,7 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
       for (int k = 0; k < NQ; ++k)
         if (k <= li) gp->L[tri(li, k)] = Lr[k];
     }
+#if FFDDP_KN_SCHUR
     // y1 = L^-1 (u - tau); free: a = L^-T y1.  Contact (the KKT by its Schur
     // complement): Y = L^-1 Jc^T, S = Y'Y + eps, yl = S^-1 (gamma + Y'y1),
     // a = L^-T (y1 - Y yl), lambda = -yl: one backward substitution, and the
@@ -331,6 +340,50 @@ __device__ __forceinline__ double node_primal_g8(const DevConsts& C, int mode, b
       for (int r = 0; r < NC; ++r) lam[r] = -yl[r];
     }
     a = g8_bwd_all<true>(Lr, y1, li);
+#else
+    // FFDDP_KN_SCHUR=0: the two-solve form (a = af + M^-1 Jc^T (-yl),
+    // af = M^-1 (u - tau), Schur sums across the group's lanes)
+    const double af = g8_solve<true>(Lr, u - tau, li);
+    if (surface) {
+      constexpr int c0 = NC == 1 ? 2 : 0;
+      const double pstar[3] = {ref[0], ref[1], ref[2] - C.z_press};
+      double rel[3] = {pee[0] - o[0], pee[1] - o[1], pee[2] - o[2]};
+      double jcol[3];
+      cross3(z, rel, jcol);
+      double Jc[3], Y[3], gam[3];
+#pragma unroll
+      for (int r = 0; r < NC; ++r) {
+        Jc[r] = J ? jcol[c0 + r] : 0.0;
+        gam[r] = ap0[c0 + r] + C.Kp * (pee[c0 + r] - pstar[c0 + r]) + C.Kd * vp[c0 + r];
+        Y[r] = g8_fwd<true>(Lr, Jc[r], li);
+        if (J) {
+          gp->Jc[r][li] = Jc[r];
+          gp->Y[r][li] = Y[r];
+        }
+      }
+      double S[6], yl[3];
+#pragma unroll
+      for (int r = 0; r < NC; ++r) {
+#pragma unroll
+        for (int s2 = 0; s2 <= r; ++s2) S[tri(r, s2)] = g8_sum(J ? Y[r] * Y[s2] : 0.0) + (r == s2 ? C.eps : 0.0);
+        yl[r] = gam[r] + g8_sum(J ? Jc[r] * af : 0.0);
+      }
+      chol_packed<NC>(S);
+      if (li == 0) {
+#pragma unroll
+        for (int e = 0; e < NC * (NC + 1) / 2; ++e) gp->Ls[e] = S[e];
+      }
+      chol_solve<NC>(S, yl);
+      double rhs = 0.0;
+#pragma unroll
+      for (int r = 0; r < NC; ++r) rhs += Jc[r] * (-yl[r]);
+      a = af + g8_solve<true>(Lr, rhs, li);
+#pragma unroll
+      for (int r = 0; r < NC; ++r) lam[r] = -yl[r];
+    } else {
+      a = af;
+    }
+#endif
   }
   if (!J) a = 0.0;
   if (J) gp->a[li] = a;

@@ -27,6 +27,12 @@
 
 #pragma clang fp contract(off)
 
+// the rollout's contact solve: one backward substitution through the Schur
+// complement (1) or two solves (0)
+#ifndef FFDDP_LS_SCHUR
+#define FFDDP_LS_SCHUR 1
+#endif
+
 namespace ffddp {
 
 // ---- scalar helpers, explicit fma ----
@@ -529,6 +535,7 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K,
         for (int k = i + 1; k < NC; ++k) s = fma(-S[tri(k, i)], yl[k], s);
         yl[i] = s * S[tri(i, i)];
       }
+#if FFDDP_LS_SCHUR
       // a = L^-T (y1 - Y yl), lambda = -yl
       double y2[NQ];
 #pragma unroll
@@ -539,6 +546,15 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K,
         y2[k] = s;
       }
       a = ls_bwd<ROW>(Lt, y2, li);
+#else
+      // two solves: a = L^-T y1 + M^-1 Jc^T (-yl)
+      double rhs = 0.0;
+#pragma unroll
+      for (int r = 0; r < NC; ++r) rhs = fma(J ? jcol[c0 + r] : 0.0, -yl[r], rhs);
+      double y3[NQ];
+      ls_fwd<ROW>(Lr, rhs, y3);
+      a = ls_bwd<ROW>(Lt, y1, li) + ls_bwd<ROW>(Lt, y3, li);
+#endif
 #pragma unroll
       for (int r = 0; r < NC; ++r) lam[r] = -yl[r];
     } else {

@@ -16,7 +16,8 @@ significands the two forms agree to ~1e-15).
 max |impl - ext| / max(1, max |ext|) over xs, us, K, cost; one JSON line per
 case.  Oracle / test infrastructure only.
 
-usage: python tools/ext_budget.py OUT.jsonl [GPU.npz] [CASE-NAME-PREFIX]
+usage: python tools/ext_budget.py OUT.jsonl [GPU.npz[,GPU2.npz,...]] [CASE-NAME-PREFIX]
+(several npz: one "gpu:<file stem>" implementation each, e.g. library variants)
 """
 from __future__ import annotations
 
@@ -103,7 +104,11 @@ def main():
     from oracle import cpu_fddp
 
     out_path = Path(sys.argv[1])
-    gpu = dict(np.load(sys.argv[2])) if len(sys.argv) > 2 and sys.argv[2] else None
+    gpus = {}
+    if len(sys.argv) > 2 and sys.argv[2]:
+        paths = sys.argv[2].split(",")
+        for pth in paths:
+            gpus["gpu" if len(paths) == 1 else "gpu:" + Path(pth).stem] = dict(np.load(pth))
     lines = []
     with ProcessPoolExecutor(max_workers=8, mp_context=get_context("spawn")) as ex:
         only = sys.argv[3] if len(sys.argv) > 3 else ""
@@ -118,21 +123,22 @@ def main():
             res = list(ex.map(_solve, jobs))
             f64, ext, f64s = res[:B], res[B:2 * B], res[2 * B:]
             cpu = cpu_fddp.solve_batch(_abi.robot_struct(), cfg.to_struct(), b, nthreads=4)
-            rec = {"case": case[0], "B": B, "N": case[4], "same_path": [], "oracle": {}, "oracle_solve": {}, "cpu": {},
-                   "gpu": {}}
+            rec = {"case": case[0], "B": B, "N": case[4], "same_path": [], "oracle": {}, "oracle_solve": {}, "cpu": {}}
             impls = {"oracle": {k: np.stack([r[k] for r in f64]) for k in ("xs", "us", "K")},
                      "oracle_solve": {k: np.stack([r[k] for r in f64s]) for k in ("xs", "us", "K")},
                      "cpu": {k: cpu[k] for k in ("xs", "us", "K")}}
             impls["oracle"]["cost"] = np.array([r["cost"] for r in f64])
             impls["oracle_solve"]["cost"] = np.array([r["cost"] for r in f64s])
             impls["cpu"]["cost"] = cpu["cost"]
-            if gpu is not None and f"{case[0]}/xs" in gpu:
-                impls["gpu"] = {k: gpu[f"{case[0]}/{k}"] for k in ("xs", "us", "K", "cost")}
+            for gname, gpu in gpus.items():
+                if f"{case[0]}/xs" in gpu:
+                    impls[gname] = {k: gpu[f"{case[0]}/{k}"] for k in ("xs", "us", "K", "cost")}
             for i in range(B):
                 same = (f64[i]["iter"] == ext[i]["iter"] and f64[i]["trials"] == ext[i]["trials"]
                         and f64[i]["ok"] == ext[i]["ok"])
                 rec["same_path"].append(bool(same))
             for name, im in impls.items():
+                rec.setdefault(name, {})
                 for k in ("xs", "us", "K", "cost"):
                     e = max(err(im[k][i], ext[i][k]) for i in range(B) if rec["same_path"][i]) \
                         if any(rec["same_path"]) else None
@@ -140,10 +146,10 @@ def main():
                 rec[name]["K_elem"] = max(err_elem(im["K"][i], ext[i]["K"]) for i in range(B) if rec["same_path"][i]) \
                     if any(rec["same_path"]) else None
             # oracle vs cpu vs gpu pairwise, for reference
-            if "gpu" in impls:
+            for gname in (g for g in impls if g.startswith("gpu")):
                 for ref in ("oracle", "oracle_solve"):
-                    rec[f"gpu_vs_{ref}"] = {k: max(err(impls["gpu"][k][i], impls[ref][k][i]) for i in range(B))
-                                            for k in ("xs", "us", "K", "cost")}
+                    rec[f"{gname}_vs_{ref}"] = {k: max(err(impls[gname][k][i], impls[ref][k][i]) for i in range(B))
+                                                for k in ("xs", "us", "K", "cost")}
             rec["seconds"] = time.time() - t0
             print(json.dumps(rec), flush=True)
             lines.append(rec)

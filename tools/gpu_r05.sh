@@ -7,6 +7,7 @@
 #   nccl    one-process RCCL group: bench at B=4096 / 512 with --gather none / costs / full
 #   queue   RCCL communicator vs the slice streams' hardware queues (tools/nccl_queue.py)
 #   tests   pytest -m gpu with the parity log
+#   ext     error-budget cases through each library in $EXTLIBS -> ext_<lib>.npz (tools/ext_budget.py reads them)
 #   bench   one default bench line
 #   ab      lib/base vs the in-tree library, then line-search layout thresholds (FFDDP_LS_ROW_MAX)
 #   forced  bench with a forced one-process RCCL group vs without (gather none)
@@ -38,9 +39,13 @@ for st in $STEPS; do
             tail -1 $O/q_${m}_${B}_$g.log | tee -a $O/queue.txt
           done; done; done ;;
     tests) rm -f $O/parity.jsonl
-        FFDDP_PARITY_LOG=$O/parity.jsonl timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+        FFDDP_PARITY_LOG=$O/parity.jsonl timeout -k 10 1000 python3 -u -m pytest tests -m gpu ${TESTX--x} -v --timeout 300 \
           --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
         tail -1 $O/gpu_tests.log ;;
+    ext) for L in ${EXTLIBS:-base main}; do
+          if [ $L = main ]; then LIB=$R/franka-force-feedback-mpc_amd/lib/libffddp.so; else LIB=$R/franka-force-feedback-mpc_amd/lib/$L/libffddp.so; fi
+          FFDDP_LIB=$LIB timeout -k 10 200 python3 tools/ext_budget_gpu.py $O/ext_$L.npz > $O/ext_$L.log 2>&1 || { tail -20 $O/ext_$L.log; exit 1; }
+        done ;;
     bench) timeout -k 10 400 python3 bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
         tail -1 $O/bench.log | cut -c1-300 ;;
     ab) STEPS=10 BATCHES="${ABB:-4096 1024 512}" bash tools/ab_libs.sh $TAG/ab ${LIBS:-base main} ;;
