@@ -8,6 +8,8 @@
 #   queue   RCCL communicator vs the slice streams' hardware queues (tools/nccl_queue.py)
 #   tests   pytest -m gpu with the parity log
 #   ext     error-budget cases through each library in $EXTLIBS -> ext_<lib>.npz (tools/ext_budget.py reads them)
+#   sq      SQ counter passes at B=4096 and B=512 (tools/pmc_sq2.sh)
+#   prof    kernel-trace stats (timed and single-stream), FETCH/WRITE traffic, full bench line (tools/gpu_prof.sh)
 #   bench   one default bench line
 #   ab      lib/base vs the in-tree library, then line-search layout thresholds (FFDDP_LS_ROW_MAX)
 #   forced  bench with a forced one-process RCCL group vs without (gather none)
@@ -46,6 +48,11 @@ for st in $STEPS; do
           if [ $L = main ]; then LIB=$R/franka-force-feedback-mpc_amd/lib/libffddp.so; else LIB=$R/franka-force-feedback-mpc_amd/lib/$L/libffddp.so; fi
           FFDDP_LIB=$LIB timeout -k 10 200 python3 tools/ext_budget_gpu.py $O/ext_$L.npz > $O/ext_$L.log 2>&1 || { tail -20 $O/ext_$L.log; exit 1; }
         done ;;
+    sq) $R/tools/pmc_sq2.sh $TAG/sq4096 > $O/sq4096.log 2>&1 || { tail -20 $O/sq4096.log; exit 1; }
+        BENCH_ARGS="--batch 512" SQ_CONFIG=classical/normal_1d/B512/N30 $R/tools/pmc_sq2.sh $TAG/sq512 > $O/sq512.log 2>&1 || { tail -20 $O/sq512.log; exit 1; }
+        head -12 $O/sq4096/summary.txt; head -12 $O/sq512/summary.txt ;;
+    prof) bash $R/tools/gpu_prof.sh $TAG/prof skip-tests > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+        tail -3 $O/prof.log | cut -c1-300 ;;
     bench) timeout -k 10 400 python3 bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
         tail -1 $O/bench.log | cut -c1-300 ;;
     ab) STEPS=10 BATCHES="${ABB:-4096 1024 512}" bash tools/ab_libs.sh $TAG/ab ${LIBS:-base main} ;;
