@@ -63,6 +63,13 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 #ifndef FFDDP_QSPARE
 #define FFDDP_QSPARE 1
 #endif
+// BW_PF_LATE: when k_backward_w issues the loads of the next node's record:
+// at the top of the node (0), or after phase D with the record staged into
+// LDS at the end of the node (S.R is dead after phase C), so the prefetch
+// registers are not live across the gains (1: FF only, 2: both variants)
+#ifndef BW_PF_LATE
+#define BW_PF_LATE 1
+#endif
 #ifndef BW_WAVES
 #define BW_WAVES 1
 #endif
@@ -105,6 +112,9 @@ struct Dev {
 // wave per SIMD (the 1-wave/SIMD line search with 4 trials) ran its active
 // waves in two dispatch rounds.  k_accept appends the instances that
 // continue to the other list; k_backward_w zeroes that list's length first.
+// a global-memory pointer (address space 1): stays one after an opaque asm
+template <class T> using gptr = __attribute__((address_space(1))) T*;
+
 struct ActiveList {
   const int* list;
   int n;
@@ -761,6 +771,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   using S_t = BwW<FF>;
   constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
   constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane
+  constexpr bool PF_LATE = BW_PF_LATE == 2 || (BW_PF_LATE == 1 && FF);
   const DevConsts& C = *Cg;
   const int N = C.N;
   const int l = threadIdx.x;
@@ -769,7 +780,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   // active-count ranges: (late_max, B] this variant, (w2_max, late_max] LATE,
   // [1, w2_max] the two-wave k_backward_w2
   if ((int)blockIdx.x >= al.n || (LATE ? (al.n > late_max || al.n <= w2_max) : al.n <= late_max)) return;
-  const int b = al.list[blockIdx.x];
+  // one instance per block: the index (and every address derived from it) in SGPRs
+  const int b = __builtin_amdgcn_readfirstlane(al.list[blockIdx.x]);
   InstState* st = d.st + b;
   if (st->done) return;
 #ifdef FFDDP_PHASE_PROF
@@ -781,6 +793,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   const bool use_qp = C.use_box && feas;
   const double dt = C.dt, dt2 = C.dt * C.dt, alpha = C.alpha, beta = C.beta;
   const double* recb = d.rec_buf + (long)b * (N + 1) * REC;
+  // this instance's slices of the state arrays (uniform bases, 32-bit lane
+  // offsets in the node loop)
+  const double* fs_i = d.fs + (long)b * (N + 1) * NX;
+  const double* k_i = d.k + (long)b * N * NU;
+  const double* us_i = d.us + (long)b * N * NU;
+  double* K_i = d.K + (long)b * N * NU * NX;
+  double* kw_i = d.k + (long)b * N * NU;
+  double* w_i = d.w + (long)b * (N + 1) * NX;
   if (st->recalc) {
     double c = 0.0;
     for (int t = l; t <= N; t += 64) c += recb[(long)t * REC + rec_off_cost(NX)];
@@ -819,14 +839,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   for (;;) {
     dg = dq = stop = ffl = 0.0;
     bool failed = false;
+    // the bases, opaque per pass: the addresses of the terminal node's
+    // inputs and of the first prefetch are then formed in each pass instead
+    // of being hoisted out of the retry loop and held across it (FF: 15 of
+    // them spilled, classical 8 more VGPRs)
+    gptr<const double> rbase = (gptr<const double>)recb, fsb = (gptr<const double>)fs_i,
+                       kb = (gptr<const double>)k_i, usb = (gptr<const double>)us_i;
+    gptr<double> wb = (gptr<double>)w_i;
+    asm volatile("" : "+s"(rbase), "+s"(fsb), "+s"(kb), "+s"(usb), "+s"(wb));
     // ---- terminal node: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N) ----
     {
-      const double* rT = recb + (long)N * REC;
+      gptr<const double> rT = rbase + (long)N * REC;
       for (int e = l; e < NX * NX; e += 64) {
         const int i = e / NX, j = e % NX;
         S.V[e] = rT[rec_off_Lxx(NX) + e] + (i == j ? preg : 0.0);
       }
-      S.fs[l] = d.fs[((long)b * (N + 1) + N) * NX + (l < NX ? l : NX - 1)];
+      S.fs[l] = fsb[N * NX + (l < NX ? l : NX - 1)];
     }
     lds_sync();
     // Prefetch of the next node's inputs: unconditional loads from clamped
@@ -836,24 +864,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
     const int lx = l < NX ? l : NX - 1, lu = l < NU ? l : NU - 1;
     double pf[NPF];
     {
-      const double* r1 = recb + (long)(N - 1) * REC;
+      gptr<const double> r1 = rbase + (long)(N - 1) * REC;
 #pragma unroll
       for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
     }
-    double pfs = d.fs[((long)b * (N + 1) + N - 1) * NX + lx];
-    double pkp = d.k[((long)b * N + N - 1) * NU + lu];
-    double pus = d.us[((long)b * N + N - 1) * NU + lu];
+    double pfs = fsb[(N - 1) * NX + lx];
+    double pkp = kb[(N - 1) * NU + lu];
+    double pus = usb[(N - 1) * NU + lu];
     {
       double cdg = 0.0, cdq = 0.0;
       if (l < NX) {
-        const double* rT = recb + (long)N * REC;
+        gptr<const double> rT = rbase + (long)N * REC;
         double vfs = 0.0;
         for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
         const double fj = S.fs[l];
         ffl = fabs(fj);
         const double vx = rT[rec_off_Lx(NX) + l] + (feas ? 0.0 : vfs);
         if (!feas) {
-          d.w[((long)b * (N + 1) + N) * NX + l] = vfs;
+          wb[N * NX + l] = vfs;
           cdg = -vx * fj;
           cdq = fj * vfs;
         }
@@ -863,21 +891,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       dq += cdq;
     }
     lds_sync();
+    if (PF_LATE) {
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];  // record N-1; the node loop stages the rest
+    }
     for (int t = N - 1; t >= 0; --t) {
       // ---- stage record t (prefetched) ; start loading record t-1 ----
+      if (!PF_LATE) {
 #pragma unroll
-      for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
+        for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
+      }
       S.fs[l] = pfs;
       S.kp[l] = pkp;
       S.uu[l] = pus;
       {
         const int tn = t > 0 ? t - 1 : 0;
-        const double* r1 = recb + (long)tn * REC;
+        if (!PF_LATE) {
 #pragma unroll
-        for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
-        pfs = d.fs[((long)b * (N + 1) + tn) * NX + lx];
-        pkp = d.k[((long)b * N + tn) * NU + lu];
-        pus = d.us[((long)b * N + tn) * NU + lu];
+          for (int k = 0; k < NPF; ++k) pf[k] = recb[(unsigned)(tn * REC + ((l + 64 * k < REC) ? l + 64 * k : REC - 1))];
+        }
+        pfs = fs_i[(unsigned)(tn * NX + lx)];
+        pkp = k_i[(unsigned)(tn * NU + lu)];
+        pus = us_i[(unsigned)(tn * NU + lu)];
       }
       // no barrier here: phase A reads only V / Vx, and its closing barrier
       // publishes the staged record and gap before phase B reads them
@@ -1013,6 +1048,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       }
       lds_sync();
       PP(4);
+      if (PF_LATE) {  // the next node's record (S.R is dead after phase C)
+        const int tn = t > 0 ? t - 1 : 0;
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) pf[k] = recb[(unsigned)(tn * REC + ((l + 64 * k < REC) ? l + 64 * k : REC - 1))];
+      }
       // ---- phase E: K columns (and k for LLT) ----
       if (l < NX || (!use_qp && l == NX)) {
         double col[NU];
@@ -1025,11 +1065,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         }
         chol_solve<NU>(S.L, col);
         if (l < NX) {
-          double* Kt = d.K + ((long)b * N + t) * NU * NX;
 #pragma unroll
           for (int c = 0; c < NU; ++c) {
             S.K[c * NX + l] = col[c];
-            Kt[c * NX + l] = col[c];
+            K_i[(unsigned)((t * NU + c) * NX + l)] = col[c];
           }
         } else {
 #pragma unroll
@@ -1070,7 +1109,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         badv |= bad(fabs(vx)) ? 1 : 0;
         ffl = fmax(ffl, fabs(S.fs[l]));
         if (!feas) {
-          d.w[((long)b * (N + 1) + t) * NX + l] = vfs;
+          w_i[(unsigned)(t * NX + l)] = vfs;
           cdg -= vx * S.fs[l];
           cdq += S.fs[l] * vfs;
         }
@@ -1082,7 +1121,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
           cdg += qu * kl;
           cdq -= kl * quk;
           cst += qu * qu;
-          d.k[((long)b * N + t) * NU + l] = kl;
+          kw_i[(unsigned)(t * NU + l)] = kl;
         }
         S.Vx[l] = vx;  // old Vx is dead after phase B
       }
@@ -1094,6 +1133,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       dg += cdg;
       dq += cdq;
       stop += cst;
+      if (PF_LATE) {
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
+      }
       lds_sync();
       PP(7);
     }
@@ -1170,7 +1213,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (blockIdx.x == 0 && tid == 0) d.acnt[cur ^ 1] = d.acnt[2 + (cur ^ 1)] = 0;  // the list k_accept builds
   const ActiveList al = active_list(d, cur);
   if ((int)blockIdx.x >= al.n || al.n > w2_max) return;
-  const int b = al.list[blockIdx.x];
+  // one instance per block: the index (and every address derived from it) in SGPRs
+  const int b = __builtin_amdgcn_readfirstlane(al.list[blockIdx.x]);
   InstState* st = d.st + b;
   if (st->done) return;
 #ifdef FFDDP_PHASE_PROF
@@ -1183,6 +1227,14 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const bool use_qp = C.use_box && feas;
   const double dt = C.dt, dt2 = C.dt * C.dt, alpha = C.alpha, beta = C.beta;
   const double* recb = d.rec_buf + (long)b * (N + 1) * REC;
+  // this instance's slices of the state arrays (uniform bases, 32-bit lane
+  // offsets in the node loop)
+  const double* fs_i = d.fs + (long)b * (N + 1) * NX;
+  const double* k_i = d.k + (long)b * N * NU;
+  const double* us_i = d.us + (long)b * N * NU;
+  double* K_i = d.K + (long)b * N * NU * NX;
+  double* kw_i = d.k + (long)b * N * NU;
+  double* w_i = d.w + (long)b * (N + 1) * NX;
   if (st->recalc && wv == 0) {
     double c = 0.0;
     for (int t = l; t <= N; t += 64) c += recb[(long)t * REC + rec_off_cost(NX)];
@@ -1221,43 +1273,48 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (;;) {
     dg = dq = stop = ffl = 0.0;
     bool failed = false;
+    // the bases, opaque per pass (k_backward_w)
+    gptr<const double> rbase = (gptr<const double>)recb, fsb = (gptr<const double>)fs_i,
+                       kb = (gptr<const double>)k_i, usb = (gptr<const double>)us_i;
+    gptr<double> wb = (gptr<double>)w_i;
+    asm volatile("" : "+s"(rbase), "+s"(fsb), "+s"(kb), "+s"(usb), "+s"(wb));
     // ---- terminal node: Vxx = Lxx_N + preg I ; Vx = Lx_N (+ Vxx fs_N) ----
     {
-      const double* rT = recb + (long)N * REC;
+      gptr<const double> rT = rbase + (long)N * REC;
       for (int e = tid; e < NX * NX; e += 128) {
         const int i = e / NX, j = e % NX;
         S.V[e] = rT[rec_off_Lxx(NX) + e] + (i == j ? preg : 0.0);
       }
-      if (wv == 0) S.fs[l] = d.fs[((long)b * (N + 1) + N) * NX + lx];
+      if (wv == 0) S.fs[l] = fsb[N * NX + lx];
     }
     // wave 1: record N-1 into LDS now, the prefetch of record N-2 in flight
     double pf[NPF];
     if (wv == 1) {
-      const double* r1 = recb + (long)(N - 1) * REC;
+      gptr<const double> r1 = rbase + (long)(N - 1) * REC;
 #pragma unroll
       for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
 #pragma unroll
       for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
-      const double* r2 = recb + (long)(N > 1 ? N - 2 : 0) * REC;
+      gptr<const double> r2 = rbase + (long)(N > 1 ? N - 2 : 0) * REC;
 #pragma unroll
       for (int k = 0; k < NPF; ++k) pf[k] = r2[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
     }
     lds_sync();
     double pfs = 0.0, pkp = 0.0, pus = 0.0;
     if (wv == 0) {
-      pfs = d.fs[((long)b * (N + 1) + N - 1) * NX + lx];
-      pkp = d.k[((long)b * N + N - 1) * NU + lu];
-      pus = d.us[((long)b * N + N - 1) * NU + lu];
+      pfs = fsb[(N - 1) * NX + lx];
+      pkp = kb[(N - 1) * NU + lu];
+      pus = usb[(N - 1) * NU + lu];
       double cdg = 0.0, cdq = 0.0;
       if (l < NX) {
-        const double* rT = recb + (long)N * REC;
+        gptr<const double> rT = rbase + (long)N * REC;
         double vfs = 0.0;
         for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
         const double fj = S.fs[l];
         ffl = fabs(fj);
         const double vx = rT[rec_off_Lx(NX) + l] + (feas ? 0.0 : vfs);
         if (!feas) {
-          d.w[((long)b * (N + 1) + N) * NX + l] = vfs;
+          wb[N * NX + l] = vfs;
           cdg = -vx * fj;
           cdq = fj * vfs;
         }
@@ -1284,7 +1341,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         badv |= bad(fabs(vx)) ? 1 : 0;
         ffl = fmax(ffl, fabs(fsg[l]));
         if (!feas) {
-          d.w[((long)b * (N + 1) + tg) * NX + l] = vfs;
+          w_i[(unsigned)(tg * NX + l)] = vfs;
           cdg -= vx * fsg[l];
           cdq += fsg[l] * vfs;
         }
@@ -1296,7 +1353,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           cdg += qu * kl;
           cdq -= kl * quk;
           cst += qu * qu;
-          d.k[((long)b * N + tg) * NU + l] = kl;
+          kw_i[(unsigned)(tg * NU + l)] = kl;
         }
         S.Vx[l] = vx;  // old Vx is dead after phase B
       }
@@ -1321,9 +1378,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         S.kp[l] = pkp;
         S.uu[l] = pus;
         const int tn = t > 0 ? t - 1 : 0;
-        pfs = d.fs[((long)b * (N + 1) + tn) * NX + lx];
-        pkp = d.k[((long)b * N + tn) * NU + lu];
-        pus = d.us[((long)b * N + tn) * NU + lu];
+        pfs = fs_i[(unsigned)(tn * NX + lx)];
+        pkp = k_i[(unsigned)(tn * NU + lu)];
+        pus = us_i[(unsigned)(tn * NU + lu)];
         if (t < N - 1) {
           phase_g(t + 1);
           // z below reads Vx entries other lanes of this wave just wrote
@@ -1484,9 +1541,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
           const int tn = t > 1 ? t - 2 : 0;
-          const double* r1 = recb + (long)tn * REC;
 #pragma unroll
-          for (int k = 0; k < NPF; ++k) pf[k] = r1[(l + 64 * k < REC) ? l + 64 * k : REC - 1];
+          for (int k = 0; k < NPF; ++k) pf[k] = recb[(unsigned)(tn * REC + ((l + 64 * k < REC) ? l + 64 * k : REC - 1))];
         }
         // Speculative gains on wave 1: the factor of the full set (Quu, or
         // Quu + qp_reg I as BoxQP factors an empty clamped set: the same
@@ -1520,7 +1576,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
             chol_solve<NU>(S.L1, col);
             if (l < NX) {
-              double* Kt = d.K + ((long)b * N + t) * NU * NX;
+              double* Kt = K_i + (unsigned)(t * NU * NX);
 #pragma unroll
               for (int c = 0; c < NU; ++c) {
                 S.K[c * NX + l] = col[c];
@@ -1562,7 +1618,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         chol_solve<NU>(S.L, col);
         if (l < NX) {
-          double* Kt = d.K + ((long)b * N + t) * NU * NX;
+          double* Kt = K_i + (unsigned)(t * NU * NX);
 #pragma unroll
           for (int c = 0; c < NU; ++c) {
             S.K[c * NX + l] = col[c];

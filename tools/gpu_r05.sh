@@ -12,6 +12,7 @@
 #   prof    kernel-trace stats (timed and single-stream), FETCH/WRITE traffic, full bench line (tools/gpu_prof.sh)
 #   bench   one default bench line
 #   ab      lib/base vs the in-tree library, then line-search layout thresholds (FFDDP_LS_ROW_MAX)
+#   abff    the same A/B for the force-feedback variant (B = 4096 / 1024)
 #   forced  bench with a forced one-process RCCL group vs without (gather none)
 #   small   configs[4] per-GPU shape (N=100 point3d B=1024) and the C1 tick breakdown, lib/base vs in-tree
 #   quick   short bench lines at B = 4096 / 1024 / 512 (no extras)
@@ -56,6 +57,7 @@ for st in $STEPS; do
     bench) timeout -k 10 400 python3 bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
         tail -1 $O/bench.log | cut -c1-300 ;;
     ab) STEPS=10 BATCHES="${ABB:-4096 1024 512}" bash tools/ab_libs.sh $TAG/ab ${LIBS:-base main} ;;
+    abff) STEPS=10 BATCHES="${ABB:-4096 1024}" BENCH_ARGS="--variant ff" bash tools/ab_libs.sh $TAG/abff ${LIBS:-base main} ;;
     abrow) STEPS=10 BATCHES="4096 1024 512" bash tools/ab_env.sh $TAG/abe "FFDDP_LS_ROW_MAX=0" "-" "FFDDP_LS_ROW_MAX=128" "FFDDP_LS_ROW_MAX=1024" ;;
     forced) for B in 4096 512; do
           timeout -k 10 200 python3 bench.py --batch $B --force-collective --gather none --steps 20 --warmup 3 \
