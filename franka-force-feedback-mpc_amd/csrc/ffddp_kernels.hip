@@ -68,7 +68,7 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 // LDS at the end of the node (S.R is dead after phase C), so the prefetch
 // registers are not live across the gains (1: FF only, 2: both variants)
 #ifndef BW_PF_LATE
-#define BW_PF_LATE 1
+#define BW_PF_LATE 0
 #endif
 #ifndef BW_WAVES
 #define BW_WAVES 1
@@ -1786,8 +1786,11 @@ __device__ __forceinline__ int ls_row_bcast0(int v) {  // lane 0 of the row into
   return __builtin_amdgcn_update_dpp(v, v, 0x150, 0xf, 0xf, false);
 }
 #pragma clang fp contract(off)
+#ifndef FW_WPE
+#define FW_WPE 1  // waves per SIMD of the two-groups-per-row layout's register budget
+#endif
 template <int NC, bool FF, bool ROW>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_forward_g8(const DevConsts* __restrict__ Cg, Dev d,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW_WPE))) void k_forward_g8(const DevConsts* __restrict__ Cg, Dev d,
                                                    const double* __restrict__ x0,
                                                    const double* __restrict__ node_ref,
                                                    const double* __restrict__ inst_ref,
