@@ -58,8 +58,14 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 #ifndef QC_UNROLL
 #define QC_UNROLL 1
 #endif
-// FFDDP_QSPARE: phase C's spare lanes (past the last Q entry) store to a
-// slot of their own (1), or rewrite entry (0, 0) with its owner's bits (0)
+// FFDDP_QSPARE: phase C's spare lanes (past the last Q entry) compute entry
+// (0, 0) and store it to a slot of their own where phase C's passes are
+// unrolled (1: the unrolled copies may contract products into FMAs
+// differently, and a rewrite of (0, 0) could then race with different
+// bits), or always (2); with the rolled loop (1, k_backward_w's throughput
+// variants) every pass runs the same instructions, so a spare lane rewrites
+// (0, 0) with its owner's bits and no address select is needed (FF B = 4096:
+// backward 934 -> 917 us per launch).  0: never
 #ifndef FFDDP_QSPARE
 #define FFDDP_QSPARE 1
 #endif
@@ -112,6 +118,10 @@ struct Dev {
 // wave per SIMD (the 1-wave/SIMD line search with 4 trials) ran its active
 // waves in two dispatch rounds.  k_accept appends the instances that
 // continue to the other list; k_backward_w zeroes that list's length first.
+// marks accumulator registers a0..a39 used, so the kernel's register
+// allocation (and its SIMD occupancy) includes them
+#define RESERVE_AGPR40() asm volatile("" ::: "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39")
+
 // a global-memory pointer (address space 1): stays one after an opaque asm
 template <class T> using gptr = __attribute__((address_space(1))) T*;
 
@@ -784,6 +794,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   const int b = __builtin_amdgcn_readfirstlane(al.list[blockIdx.x]);
   InstState* st = d.st + b;
   if (st->done) return;
+  // LATE runs a slice's latency-bound tail: its wave should have its SIMD to
+  // itself.  FF's pass fits 254 VGPRs, which would let another slice's
+  // k_node wave (253) share the SIMD (FF B = 1024: backward 306 -> 330 us
+  // per launch); 40 reserved AGPRs keep the allocation above 256
+  if (LATE && FF) RESERVE_AGPR40();
 #ifdef FFDDP_PHASE_PROF
   const bool pp_on = (b == 0);
 #endif
@@ -821,6 +836,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   // phase C unroll: full in the classical latency variant; FF's 7 passes
   // unrolled spill into AGPRs (1.5 % slower at B=1024), so not there
   constexpr int QC_N = LATE ? (FF ? 1 : NQL) : QC_UNROLL;
+  constexpr bool QSP = FFDDP_QSPARE == 2 || (FFDDP_QSPARE == 1 && QC_N > 1);
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 63) / 64;
   int qrc[NQL], vij[NVL];
 #pragma unroll
@@ -995,14 +1011,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-#if FFDDP_QSPARE
-          *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
-          *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
-#else
-          (void)spare;
-          S.Q[r * ND + c] = v;
-          S.Q[c * ND + r] = v;
-#endif
+          if (QSP) {
+            *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
+            *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
+          } else {
+            S.Q[r * ND + c] = v;
+            S.Q[c * ND + r] = v;
+          }
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
@@ -1253,6 +1268,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
     S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
   }
   // this lane's lower-triangle entries of Q (phase C) and V (phase F) over 128 lanes
+  constexpr bool QSP = FFDDP_QSPARE != 0;  // phase C unrolled
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 127) / 128;
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 127) / 128;
   int qrc[NQL], vij[NVL];
@@ -1485,14 +1501,13 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-#if FFDDP_QSPARE
-          *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
-          *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
-#else
-          (void)spare;
-          S.Q[r * ND + c] = v;
-          S.Q[c * ND + r] = v;
-#endif
+          if (QSP) {
+            *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
+            *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
+          } else {
+            S.Q[r * ND + c] = v;
+            S.Q[c * ND + r] = v;
+          }
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
