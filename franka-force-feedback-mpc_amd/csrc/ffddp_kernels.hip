@@ -982,9 +982,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 #pragma unroll QC_N
       for (int k = 0; k < NQL; ++k) {
         // no range guard: a lane past the last entry computes entry (0, 0)
-        // (qrc's default) and stores it to the spare slot S.qspare (the
-        // address is selected, not the branch), so the passes need no
-        // divergent branch and can interleave, and no entry has two writers
+        // (qrc's default), so the passes need no divergent branch and can
+        // interleave; unrolled (QSP) it stores to the spare slot S.qspare
+        // (the address is selected, not the branch), rolled it rewrites
+        // (0, 0) with the bits lane 0 wrote (same instructions, FFDDP_QSPARE)
         {
           const int r = (qrc[k] >> 8) & 255, c = qrc[k] & 255;
           const bool spare = (qrc[k] >> 16) != 0;
