@@ -282,10 +282,8 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     # The device, the null stream and the solver's slice streams come first,
-    # the process group after them: streams created after RCCL's own took
-    # shared hardware queues (4 per process) and the solve ran 34 % (B=4096)
-    # to 47 % (B=512) slower with an idle communicator in the process
-    # (tools/nccl_queue.py)
+    # the process group after them (the solver is tuned to one hardware
+    # queue per slice, 4 per process; shard.prepare_device)
     torch.zeros(1, device=dev)
 
     B, N, nu = args.batch, args.horizon, 7

@@ -38,11 +38,13 @@ _RESERVED = []  # keeps the slice streams' reference alive for the process
 def prepare_device(local_rank: int):
     """The device, its null stream and the solver library's slice streams,
     created before the RCCL communicator: a process gets 4 hardware queues
-    (GPU_MAX_HW_QUEUES), the first streams get one each, and with RCCL's
-    streams created first the solver's slices shared queues (an idle
-    communicator made B=4096 solves 34 % slower and B=512 47 %,
-    tools/nccl_queue.py).  A one-instance handle holds the
-    library's per-device stream pool for the life of the process."""
+    (GPU_MAX_HW_QUEUES) and the solver is tuned to one per slice, so its
+    streams are claimed before RCCL creates its own.  On the round-5 head no
+    creation order measured slower on one GPU (tools/nccl_queue.py,
+    profiles/r05_nccl_queue.txt); the order is kept because
+    it does not depend on how the runtime maps streams to queues.  A
+    one-instance handle holds the library's per-device stream pool for the
+    life of the process."""
     torch.cuda.set_device(local_rank)
     torch.zeros(1, device=torch.device("cuda", local_rank))
     if not _RESERVED:

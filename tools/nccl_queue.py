@@ -3,7 +3,11 @@
 slice streams (4 hardware queues per process, GPU_MAX_HW_QUEUES)?  Runs one
 configuration per process (--mode):
   none         no process group (the one-GPU bench)
-  rccl_first   one-process nccl group created first, then the solver
+  rccl_raw     one-process nccl group created first by init_process_group
+               itself (no shard.prepare_device), then the solver: the
+               order without the fix
+  rccl_first   one-process nccl group through shard.init (which creates the
+               solver's slice streams first), then the solver
   solver_first the solver's slice streams created (one warm-up solve) before
                the nccl group
 and prints solves/s of B instances for --gather none / costs / full.
@@ -21,7 +25,7 @@ import ffddp_path  # noqa: E402,F401
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=("none", "rccl_first", "solver_first", "bench_order", "bench_touch",
+    ap.add_argument("--mode", choices=("none", "rccl_raw", "rccl_first", "solver_first", "bench_order", "bench_touch",
                                        "bench_solver"), required=True)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--gather", choices=("none", "costs", "full"), default="none")
@@ -70,6 +74,8 @@ def main():
         torch.cuda.synchronize(dev)
     if a.mode in ("rccl_first", "solver_first"):
         shard.init("nccl", 0, 1, force=True)
+    if a.mode == "rccl_raw":
+        dist.init_process_group("nccl", device_id=dev, store=dist.HashStore(), rank=0, world_size=1)
     aff2 = len(os.sched_getaffinity(0))
     if a.mode == "bench_solver":
         solver = solver0
