@@ -12,6 +12,7 @@
 #   prof    kernel-trace stats (timed and single-stream), FETCH/WRITE traffic, full bench line (tools/gpu_prof.sh)
 #   bench   one default bench line
 #   ab      lib/base vs the in-tree library, then line-search layout thresholds (FFDDP_LS_ROW_MAX)
+#   abrnd   the same A/B in the random-x0 regime (B = 1024 / 4096)
 #   abff    the same A/B for the force-feedback variant (B = 4096 / 1024)
 #   phase   per-phase cycles of instance 0 at B = 1 and 512 (lib/prof: build with -DFFDDP_PHASE_PROF)
 #   forced  bench with a forced one-process RCCL group vs without (gather none)
@@ -60,7 +61,8 @@ for st in $STEPS; do
     ab) STEPS=10 BATCHES="${ABB:-4096 1024 512}" bash tools/ab_libs.sh $TAG/ab ${LIBS:-base main} ;;
     abff) STEPS=10 BATCHES="${ABB:-4096 1024}" BENCH_ARGS="--variant ff" bash tools/ab_libs.sh $TAG/abff ${LIBS:-base main} ;;
     phase) for B in 1 512; do echo "== prof B=$B"; FFDDP_LIB=$R/franka-force-feedback-mpc_amd/lib/prof/libffddp.so timeout -k 10 200 python3 tools/phase_prof.py $B 2>&1 | grep -v amdgpu.ids; done | tee $O/phase_prof.txt ;;
-    abrow) STEPS=10 BATCHES="4096 1024 512" bash tools/ab_env.sh $TAG/abe "FFDDP_LS_ROW_MAX=0" "-" "FFDDP_LS_ROW_MAX=128" "FFDDP_LS_ROW_MAX=1024" ;;
+    abrow) STEPS=10 BATCHES="${ABB:-4096 1024 512}" bash tools/ab_env.sh $TAG/abe ${ROWS:-"FFDDP_LS_ROW_MAX=0" "-" "FFDDP_LS_ROW_MAX=128" "FFDDP_LS_ROW_MAX=1024"} ;;
+    abrnd) STEPS=10 BATCHES="${ABB:-1024 4096}" BENCH_ARGS="--regime random" bash tools/ab_libs.sh $TAG/abrnd ${LIBS:-base main} ;;
     forced) for B in 4096 512; do
           timeout -k 10 200 python3 bench.py --batch $B --force-collective --gather none --steps 20 --warmup 3 \
             --no-cpu-baseline --no-extras --no-host-io --no-profile > $O/forced_$B.log 2>&1 || { tail -20 $O/forced_$B.log; exit 1; }
