@@ -58,17 +58,6 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 #ifndef QC_UNROLL
 #define QC_UNROLL 1
 #endif
-// FFDDP_QSPARE: phase C's spare lanes (past the last Q entry) compute entry
-// (0, 0) and store it to a slot of their own where phase C's passes are
-// unrolled (1: the unrolled copies may contract products into FMAs
-// differently, and a rewrite of (0, 0) could then race with different
-// bits), or always (2); with the rolled loop (1, k_backward_w's throughput
-// variants) every pass runs the same instructions, so a spare lane rewrites
-// (0, 0) with its owner's bits and no address select is needed (FF B = 4096:
-// backward 934 -> 917 us per launch).  0: never
-#ifndef FFDDP_QSPARE
-#define FFDDP_QSPARE 1
-#endif
 // BW_PF_LATE: when k_backward_w issues the loads of the next node's record:
 // at the top of the node (0), or after phase D with the record staged into
 // LDS at the end of the node (S.R is dead after phase C), so the prefetch
@@ -559,11 +548,16 @@ template <bool FF> struct BwW {
   int flag;
   int badw[2];  // k_backward_w2: per-wave NaN flags of phases F / G
   int clamped[NU];
-  // phase C's spare lanes store here (the last member: a slot inside the
-  // struct would shift the arrays after it, i.e. their LDS bank mapping;
-  // measured: backward 350 -> 536 us per launch at B = 4096)
-  double qspare;
 };
+
+// Phase C's entry for flat index e of a pass over the lower triangle (NQE
+// entries, the last pass starting at `last`): a lane past the last entry
+// takes an entry of that same pass, so its duplicate store is computed by the
+// same instruction from the same operands as the owner's (identical bits in
+// any unrolling or contraction), with no address select and no spare slot
+__device__ __forceinline__ int spare_entry(int e, int nqe, int last) {
+  return e < nqe ? e : last + (e - last) % (nqe - last);
+}
 
 // nonzeros of column c of I~ (the Euler identity part of [Fx Fu]):
 // returns the count and fills (row, coef) pairs.
@@ -836,15 +830,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   // phase C unroll: full in the classical latency variant; FF's 7 passes
   // unrolled spill into AGPRs (1.5 % slower at B=1024), so not there
   constexpr int QC_N = LATE ? (FF ? 1 : NQL) : QC_UNROLL;
-  constexpr bool QSP = FFDDP_QSPARE == 2 || (FFDDP_QSPARE == 1 && QC_N > 1);
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 63) / 64;
   int qrc[NQL], vij[NVL];
 #pragma unroll
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
-    const bool spare = l + 64 * k >= NQE;  // past the last entry: computes entry (0, 0), stores to S.qspare
-    if (!spare) tri_rc(l + 64 * k, r, c);
-    qrc[k] = (spare ? 1 << 16 : 0) | (r << 8) | c;
+    tri_rc(spare_entry(l + 64 * k, NQE, 64 * (NQL - 1)), r, c);
+    qrc[k] = (r << 8) | c;
   }
 #pragma unroll
   for (int k = 0; k < NVL; ++k) {
@@ -981,14 +973,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       // ---- phase C: Q lower triangle (mirrored), entries fixed per lane ----
 #pragma unroll QC_N
       for (int k = 0; k < NQL; ++k) {
-        // no range guard: a lane past the last entry computes entry (0, 0)
-        // (qrc's default), so the passes need no divergent branch and can
-        // interleave; unrolled (QSP) it stores to the spare slot S.qspare
-        // (the address is selected, not the branch), rolled it rewrites
-        // (0, 0) with the bits lane 0 wrote (same instructions, FFDDP_QSPARE)
+        // no range guard: a lane past the last entry recomputes an entry of
+        // the same (last) pass (spare_entry), so the passes need no divergent
+        // branch and can interleave
         {
           const int r = (qrc[k] >> 8) & 255, c = qrc[k] & 255;
-          const bool spare = (qrc[k] >> 16) != 0;
           double lv;
           if (r < NX)
             lv = S.R[rec_off_Lxx(NX) + r * NX + c];
@@ -1012,13 +1001,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-          if (QSP) {
-            *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
-            *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
-          } else {
-            S.Q[r * ND + c] = v;
-            S.Q[c * ND + r] = v;
-          }
+          S.Q[r * ND + c] = v;
+          S.Q[c * ND + r] = v;
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
@@ -1269,16 +1253,14 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
     S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
   }
   // this lane's lower-triangle entries of Q (phase C) and V (phase F) over 128 lanes
-  constexpr bool QSP = FFDDP_QSPARE != 0;  // phase C unrolled
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 127) / 128;
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 127) / 128;
   int qrc[NQL], vij[NVL];
 #pragma unroll
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
-    const bool spare = tid + 128 * k >= NQE;  // past the last entry: computes entry (0, 0), stores to S.qspare
-    if (!spare) tri_rc(tid + 128 * k, r, c);
-    qrc[k] = (spare ? 1 << 16 : 0) | (r << 8) | c;
+    tri_rc(spare_entry(tid + 128 * k, NQE, 128 * (NQL - 1)), r, c);
+    qrc[k] = (r << 8) | c;
   }
 #pragma unroll
   for (int k = 0; k < NVL; ++k) {
@@ -1472,13 +1454,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // ---- phase C: Q lower triangle (mirrored), entries over 128 lanes ----
 #pragma unroll
       for (int k = 0; k < NQL; ++k) {
-        // no range guard: a lane past the last entry computes entry (0, 0)
-        // (qrc's default) and stores it to the spare slot S.qspare (the
-        // address is selected, not the branch), so the passes need no
-        // divergent branch and can interleave, and no entry has two writers
+        // no range guard: a lane past the last entry recomputes an entry of
+        // the same (last) pass (spare_entry), so the passes need no divergent
+        // branch and can interleave
         {
           const int r = (qrc[k] >> 8) & 255, c = qrc[k] & 255;
-          const bool spare = (qrc[k] >> 16) != 0;
           double lv;
           if (r < NX)
             lv = S.R[rec_off_Lxx(NX) + r * NX + c];
@@ -1502,13 +1482,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-          if (QSP) {
-            *(spare ? &S.qspare : &S.Q[r * ND + c]) = v;
-            *(spare ? &S.qspare : &S.Q[c * ND + r]) = v;
-          } else {
-            S.Q[r * ND + c] = v;
-            S.Q[c * ND + r] = v;
-          }
+          S.Q[r * ND + c] = v;
+          S.Q[c * ND + r] = v;
           if (c >= NX) {
             S.H[(r - NX) * NU + (c - NX)] = v;
             S.H[(c - NX) * NU + (r - NX)] = v;
