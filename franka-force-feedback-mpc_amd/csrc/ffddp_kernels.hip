@@ -65,6 +65,16 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 #ifndef BW_PF_LATE
 #define BW_PF_LATE 0
 #endif
+// backward LDS diet (round 5): BW_DIET_UNION puts Y with the factors and M
+// with K in one slot each (FF only, BwSlots), BW_DIET_SLOTS stages the
+// per-lane inputs in n-entry arrays (lane l writes slot l mod n) instead of
+// 64-entry ones
+#ifndef BW_DIET_UNION
+#define BW_DIET_UNION 1
+#endif
+#ifndef BW_DIET_SLOTS
+#define BW_DIET_SLOTS 1
+#endif
 #ifndef BW_WAVES
 #define BW_WAVES 1
 #endif
@@ -527,27 +537,60 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Y (D' V D) lives in phases A-B, the factors L (packed masked Cholesky
+// factor, reciprocal diagonal) and L1 (k_backward_w2: wave 1's factor of the
+// full set) in D-E; M in B-C, K in D/E-G (k_backward_w2: G runs beside the
+// next node's A, still before its B).  U: one slot each for Y / {L, L1} and
+// M / K.  It saves FF's backward 1.5 KB of LDS (8 blocks per CU, with the
+// rest of the diet), but the aliasing costs the classical pass at B = 4096
+// (522k-526k vs 546k-548k solves/s without it), so only FF takes it.
+template <bool U, int NM, int NK> struct BwSlots {
+  double Y[NU * NU], L[28], L1[28], M[NM], K[NK];
+};
+template <int NM, int NK> struct BwSlots<true, NM, NK> {
+  union {
+    double Y[NU * NU];
+    struct {
+      double L[28];
+      double L1[28];
+    };
+  };
+  union {
+    double M[NM];
+    double K[NK];
+  };
+};
+
 template <bool FF> struct BwW {
   static constexpr int NX = FF ? 21 : 14;
   static constexpr int ND = NX + NU;
   static constexpr int REC = rec_words(NX);
+  // Q's distinct blocks, contiguous so that phase C stores an entry through
+  // one flat index: Qxx (full, mirrored) | Qxu (row-major, NX x 7) | H =
+  // Quu + preg I (full, mirrored); Qux and the Quu copy of the full ND x ND
+  // matrix are never read (round 5: FF 25.7 -> 19.8 KB per wave, 8 blocks
+  // per CU instead of 6)
+  static constexpr int QXU = NX * NX, QH = NX * NX + NX * NU, NQQ = NX * NX + NX * NU + NU * NU;
   double R[(REC + 63) / 64 * 64];  // staged node record (A | Lxx | Lxu | Luu | Lx | Lu | cost | lam), padded
   double V[NX * NX];  // V_xx' on entry to a node, V_xx on exit
-  double Q[ND * ND];  // [[Qxx, Qxu], [Qux, Quu + preg I]]
+  double QQ[NQQ];
   double W[NX * NU];  // V D
-  double Y[NU * NU];  // D' V D
-  double M[ND * NU];
-  double K[NU * NX];
-  double H[NU * NU];  // Quu + preg I (contiguous copy for the gains lane)
-  double L[28];       // packed (masked) Cholesky factor, reciprocal diagonal
-  double L1[28];      // k_backward_w2: wave 1's factor of the full set (speculative gains)
+  // Y lives in phases A-B, the factors in D-E: one slot
+  BwSlots<FF && BW_DIET_UNION, ND * NU, NU * NX> sl;  // Y, L, L1, M, K
   int spec;           // k_backward_w2: wave 1's K (and LLT k) from L1 are valid
   double Vx[NX], Qv[ND], kk[NU], z[NU];
-  double fs[64], kp[64], uu[64], ulb[64], uub[64];  // one slot per lane: written without lane guards
-  double fsb[2][64];  // k_backward_w2: node t's gap in slot t & 1 (staged before node t+1's phase G reads its own)
+  // staged per node by every lane without lane guards: lane l writes slot
+  // l mod n, which the lanes load from the matching index (duplicate writers
+  // store the same value)
+  double fs[BW_DIET_SLOTS ? NX : 64], kp[BW_DIET_SLOTS ? NU : 64], uu[BW_DIET_SLOTS ? NU : 64];
+  double ulb[BW_DIET_SLOTS ? NU : 64], uub[BW_DIET_SLOTS ? NU : 64];
+  double fsb[2][BW_DIET_SLOTS ? NX : 64];  // k_backward_w2: node t's gap in slot t & 1 (staged before node t+1's phase G reads its own)
   int flag;
   int badw[2];  // k_backward_w2: per-wave NaN flags of phases F / G
   int clamped[NU];
+#ifdef BW_PAD_CL
+  double pad[FF ? 1 : BW_PAD_CL];  // development: classical LDS footprint back to the round-4 size
+#endif
 };
 
 // Phase C's entry for flat index e of a pass over the lower triangle (NQE
@@ -557,6 +600,22 @@ template <bool FF> struct BwW {
 // any unrolling or contraction), with no address select and no spare slot
 __device__ __forceinline__ int spare_entry(int e, int nqe, int last) {
   return e < nqe ? e : last + (e - last) % (nqe - last);
+}
+// phase C's packed entry (r >= c): r, c and the two flat BwW::QQ indices its
+// value is stored at (Qxx mirrored; Qux stored once as Qxu[c][r - NX]; Quu
+// mirrored into H)
+template <int NX> __device__ __forceinline__ int q_entry(int r, int c) {
+  int i1, i2;
+  if (r < NX) {
+    i1 = r * NX + c;
+    i2 = c * NX + r;
+  } else if (c < NX) {
+    i1 = i2 = NX * NX + c * NU + (r - NX);
+  } else {
+    i1 = NX * NX + NX * NU + (r - NX) * NU + (c - NX);
+    i2 = NX * NX + NX * NU + (c - NX) * NU + (r - NX);
+  }
+  return (r << 27) | (c << 22) | (i1 << 11) | i2;
 }
 
 // nonzeros of column c of I~ (the Euler identity part of [Fx Fu]):
@@ -773,7 +832,7 @@ template <bool FF, bool LATE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (FF ? 2 : BW_WAVES)))) void k_backward_w(
     const DevConsts* __restrict__ Cg, Dev d, int iter, int cur, int late_max, int w2_max) {
   using S_t = BwW<FF>;
-  constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
+  constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC, QXU = S_t::QXU, QH = S_t::QH;
   constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane
   constexpr bool PF_LATE = BW_PF_LATE == 2 || (BW_PF_LATE == 1 && FF);
   const DevConsts& C = *Cg;
@@ -823,8 +882,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   int retries = 0;
   bool fail_inst = false;
   double dg = 0.0, dq = 0.0, stop = 0.0, ffl = 0.0;
-  S.ulb[l] = C.u_lb[l < NU ? l : NU - 1];
-  S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
+  S.ulb[BW_DIET_SLOTS ? l % NU : l] = C.u_lb[l % NU];
+  S.uub[BW_DIET_SLOTS ? l % NU : l] = C.u_ub[l % NU];
   // this lane's lower-triangle entries of Q (phase C) and V (phase F), fixed for the whole pass
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 63) / 64;
   // phase C unroll: full in the classical latency variant; FF's 7 passes
@@ -836,7 +895,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
     tri_rc(spare_entry(l + 64 * k, NQE, 64 * (NQL - 1)), r, c);
-    qrc[k] = (r << 8) | c;
+    qrc[k] = q_entry<NX>(r, c);
   }
 #pragma unroll
   for (int k = 0; k < NVL; ++k) {
@@ -862,14 +921,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         const int i = e / NX, j = e % NX;
         S.V[e] = rT[rec_off_Lxx(NX) + e] + (i == j ? preg : 0.0);
       }
-      S.fs[l] = fsb[N * NX + (l < NX ? l : NX - 1)];
+      S.fs[BW_DIET_SLOTS ? l % NX : l] = fsb[N * NX + l % NX];
     }
     lds_sync();
     // Prefetch of the next node's inputs: unconditional loads from clamped
     // addresses and unguarded LDS stores, so the code stays straight-line and
     // the compiler can wait on exactly these loads (a guarded store makes it
     // wait vmcnt(0), i.e. also on the previous node's K / k / w stores).
-    const int lx = l < NX ? l : NX - 1, lu = l < NU ? l : NU - 1;
+    const int lx = l % NX, lu = l % NU;  // every lane loads and stages slot l mod n
+    const int sx = BW_DIET_SLOTS ? lx : l, su = BW_DIET_SLOTS ? lu : l;
     double pf[NPF];
     {
       gptr<const double> r1 = rbase + (long)(N - 1) * REC;
@@ -909,9 +969,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 #pragma unroll
         for (int k = 0; k < NPF; ++k) S.R[l + 64 * k] = pf[k];
       }
-      S.fs[l] = pfs;
-      S.kp[l] = pkp;
-      S.uu[l] = pus;
+      S.fs[sx] = pfs;
+      S.kp[su] = pkp;
+      S.uu[su] = pus;
       {
         const int tn = t > 0 ? t - 1 : 0;
         if (!PF_LATE) {
@@ -939,7 +999,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         const int m = l / NU, n = l - (l / NU) * NU;
         const double wq = dt2 * S.V[m * NX + n] + dt * S.V[m * NX + 7 + n];
         const double wv = dt2 * S.V[(7 + m) * NX + n] + dt * S.V[(7 + m) * NX + 7 + n];
-        S.Y[l] = dt2 * wq + dt * wv;
+        S.sl.Y[l] = dt2 * wq + dt * wv;
       }
       if (l < NU) S.z[l] = dt2 * S.Vx[l] + dt * S.Vx[7 + l];
       lds_sync();
@@ -959,8 +1019,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         for (int m = 0; m < NU; ++m) {
           double h = 0.0;
 #pragma unroll
-          for (int n = 0; n < NU; ++n) h += Acol[n] * S.Y[n * NU + m];
-          S.M[c * NU + m] = (a0 * S.W[r0 * NU + m] + a1 * S.W[r1 * NU + m]) + 0.5 * h;
+          for (int n = 0; n < NU; ++n) h += Acol[n] * S.sl.Y[n * NU + m];
+          S.sl.M[c * NU + m] = (a0 * S.W[r0 * NU + m] + a1 * S.W[r1 * NU + m]) + 0.5 * h;
         }
         double qv = (c < NX) ? S.R[rec_off_Lx(NX) + c] : S.R[rec_off_Lu(NX) + c - NX];
         qv += a0 * S.Vx[r0] + a1 * S.Vx[r1];
@@ -977,7 +1037,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         // the same (last) pass (spare_entry), so the passes need no divergent
         // branch and can interleave
         {
-          const int r = (qrc[k] >> 8) & 255, c = qrc[k] & 255;
+          const int r = (qrc[k] >> 27) & 31, c = (qrc[k] >> 22) & 31;
           double lv;
           if (r < NX)
             lv = S.R[rec_off_Lxx(NX) + r * NX + c];
@@ -996,17 +1056,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
           double h1 = 0.0, h2 = 0.0;
 #pragma unroll
           for (int m = 0; m < NU; ++m) {
-            h1 += S.M[r * NU + m] * Ar[ic * 7 + m];
-            h2 += S.M[c * NU + m] * Ar[ir * 7 + m];
+            h1 += S.sl.M[r * NU + m] * Ar[ic * 7 + m];
+            h2 += S.sl.M[c * NU + m] * Ar[ir * 7 + m];
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-          S.Q[r * ND + c] = v;
-          S.Q[c * ND + r] = v;
-          if (c >= NX) {
-            S.H[(r - NX) * NU + (c - NX)] = v;
-            S.H[(c - NX) * NU + (r - NX)] = v;
-          }
+          S.QQ[(qrc[k] >> 11) & 2047] = v;
+          S.QQ[qrc[k] & 2047] = v;
         }
       }
       lds_sync();
@@ -1015,7 +1071,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       {
         double hrow[NU], Lr[NU];
 #pragma unroll
-        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.H[l * NU + j] : (l == j ? 1.0 : 0.0);
+        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.QQ[QH + l * NU + j] : (l == j ? 1.0 : 0.0);
         bool ok;
         if (!use_qp) {
 #pragma unroll
@@ -1025,9 +1081,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         } else {
           const bool v = l < NU;
           const double q = v ? S.Qv[NX + l] : 0.0;
-          const double lb = v ? S.ulb[l] - S.uu[l] : 0.0;
-          const double ub = v ? S.uub[l] - S.uu[l] : 0.0;
-          double x = v ? S.kp[l] : 0.0;
+          const double lb = v ? S.ulb[l % NU] - S.uu[l % NU] : 0.0;
+          const double ub = v ? S.uub[l % NU] - S.uu[l % NU] : 0.0;
+          double x = v ? S.kp[l % NU] : 0.0;
           int clm = 0;
           ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l);
           if (ok && v) {
@@ -1044,7 +1100,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         if (l < NU)
 #pragma unroll
           for (int j = 0; j < NU; ++j)
-            if (j <= l) S.L[tri(l, j)] = Lr[j];
+            if (j <= l) S.sl.L[tri(l, j)] = Lr[j];
       }
       lds_sync();
       PP(4);
@@ -1058,16 +1114,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         double col[NU];
         if (l < NX) {
 #pragma unroll
-          for (int c = 0; c < NU; ++c) col[c] = S.clamped[c] ? 0.0 : S.Q[l * ND + NX + c];
+          for (int c = 0; c < NU; ++c) col[c] = S.clamped[c] ? 0.0 : S.QQ[QXU + l * NU + c];
         } else {
 #pragma unroll
           for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
         }
-        chol_solve<NU>(S.L, col);
+        chol_solve<NU>(S.sl.L, col);
         if (l < NX) {
 #pragma unroll
           for (int c = 0; c < NU; ++c) {
-            S.K[c * NX + l] = col[c];
+            S.sl.K[c * NX + l] = col[c];
             K_i[(unsigned)((t * NU + c) * NX + l)] = col[c];
           }
         } else {
@@ -1086,10 +1142,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         double a1 = 0.0, a2 = 0.0;
 #pragma unroll
         for (int c = 0; c < NU; ++c) {
-          a1 += S.Q[i * ND + NX + c] * S.K[c * NX + j];
-          a2 += S.Q[j * ND + NX + c] * S.K[c * NX + i];
+          a1 += S.QQ[QXU + i * NU + c] * S.sl.K[c * NX + j];
+          a2 += S.QQ[QXU + j * NU + c] * S.sl.K[c * NX + i];
         }
-        const double v = S.Q[i * ND + j] - 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
+        const double v = S.QQ[i * NX + j] - 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
         S.V[i * NX + j] = v;
         S.V[j * NX + i] = v;
         badv |= bad(fabs(v)) ? 1 : 0;
@@ -1104,7 +1160,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
         double vx = S.Qv[l];
 #pragma unroll
-        for (int c = 0; c < NU; ++c) vx -= S.K[c * NX + l] * S.Qv[NX + c];
+        for (int c = 0; c < NU; ++c) vx -= S.sl.K[c * NX + l] * S.Qv[NX + c];
         if (!feas) vx += vfs;
         badv |= bad(fabs(vx)) ? 1 : 0;
         ffl = fmax(ffl, fabs(S.fs[l]));
@@ -1116,7 +1172,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         if (l < NU) {
           double quk = 0.0;
 #pragma unroll
-          for (int m = 0; m < NU; ++m) quk += S.H[l * NU + m] * S.kk[m];
+          for (int m = 0; m < NU; ++m) quk += S.QQ[QH + l * NU + m] * S.kk[m];
           const double qu = S.Qv[NX + l], kl = S.kk[l];
           cdg += qu * kl;
           cdq -= kl * quk;
@@ -1204,7 +1260,7 @@ template <bool FF, int WPE = 1>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void k_backward_w2(
     const DevConsts* __restrict__ Cg, Dev d, int iter, int cur, int w2_max) {
   using S_t = BwW<FF>;
-  constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC;
+  constexpr int NX = S_t::NX, ND = S_t::ND, REC = S_t::REC, QXU = S_t::QXU, QH = S_t::QH;
   constexpr int NPF = (REC + 63) / 64;  // prefetch registers per lane of wave 1
   const DevConsts& C = *Cg;
   const int N = C.N;
@@ -1249,8 +1305,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
   bool fail_inst = false;
   double dg = 0.0, dq = 0.0, stop = 0.0, ffl = 0.0;
   if (wv == 0) {
-    S.ulb[l] = C.u_lb[l < NU ? l : NU - 1];
-    S.uub[l] = C.u_ub[l < NU ? l : NU - 1];
+    S.ulb[BW_DIET_SLOTS ? l % NU : l] = C.u_lb[l % NU];
+    S.uub[BW_DIET_SLOTS ? l % NU : l] = C.u_ub[l % NU];
   }
   // this lane's lower-triangle entries of Q (phase C) and V (phase F) over 128 lanes
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 127) / 128;
@@ -1260,7 +1316,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
     tri_rc(spare_entry(tid + 128 * k, NQE, 128 * (NQL - 1)), r, c);
-    qrc[k] = (r << 8) | c;
+    qrc[k] = q_entry<NX>(r, c);
   }
 #pragma unroll
   for (int k = 0; k < NVL; ++k) {
@@ -1268,7 +1324,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (tid + 128 * k < NVE) tri_rc(tid + 128 * k, i, j);
     vij[k] = (i << 8) | j;
   }
-  const int lx = l < NX ? l : NX - 1, lu = l < NU ? l : NU - 1;
+  const int lx = l % NX, lu = l % NU;  // every lane loads and stages slot l mod n
+  const int sx = BW_DIET_SLOTS ? lx : l, su = BW_DIET_SLOTS ? lu : l;
   for (;;) {
     dg = dq = stop = ffl = 0.0;
     bool failed = false;
@@ -1284,7 +1341,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int i = e / NX, j = e % NX;
         S.V[e] = rT[rec_off_Lxx(NX) + e] + (i == j ? preg : 0.0);
       }
-      if (wv == 0) S.fs[l] = fsb[N * NX + lx];
+      if (wv == 0) S.fs[sx] = fsb[N * NX + lx];
     }
     // wave 1: record N-1 into LDS now, the prefetch of record N-2 in flight
     double pf[NPF];
@@ -1335,7 +1392,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * fsg[i];
         double vx = S.Qv[l];
 #pragma unroll
-        for (int c = 0; c < NU; ++c) vx -= S.K[c * NX + l] * S.Qv[NX + c];
+        for (int c = 0; c < NU; ++c) vx -= S.sl.K[c * NX + l] * S.Qv[NX + c];
         if (!feas) vx += vfs;
         badv |= bad(fabs(vx)) ? 1 : 0;
         ffl = fmax(ffl, fabs(fsg[l]));
@@ -1347,7 +1404,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (l < NU) {
           double quk = 0.0;
 #pragma unroll
-          for (int m = 0; m < NU; ++m) quk += S.H[l * NU + m] * S.kk[m];
+          for (int m = 0; m < NU; ++m) quk += S.QQ[QH + l * NU + m] * S.kk[m];
           const double qu = S.Qv[NX + l], kl = S.kk[l];
           cdg += qu * kl;
           cdq -= kl * quk;
@@ -1373,9 +1430,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // issued (vmcnt counts loads and stores in issue order, and the
         // lane-guarded stores leave the compiler only vmcnt(0)); staged
         // here, the stores have a whole node to complete before the next wait
-        S.fsb[t & 1][l] = pfs;
-        S.kp[l] = pkp;
-        S.uu[l] = pus;
+        S.fsb[t & 1][sx] = pfs;
+        S.kp[su] = pkp;
+        S.uu[su] = pus;
         const int tn = t > 0 ? t - 1 : 0;
         pfs = fs_i[(unsigned)(tn * NX + lx)];
         pkp = k_i[(unsigned)(tn * NU + lu)];
@@ -1399,7 +1456,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int m = e / NU, n = e - (e / NU) * NU;
         const double wq = dt2 * S.V[m * NX + n] + dt * S.V[m * NX + 7 + n];
         const double wv_ = dt2 * S.V[(7 + m) * NX + n] + dt * S.V[(7 + m) * NX + 7 + n];
-        S.Y[e] = dt2 * wq + dt * wv_;
+        S.sl.Y[e] = dt2 * wq + dt * wv_;
       }
       if (tid < NU) S.z[tid] = dt2 * S.Vx[tid] + dt * S.Vx[7 + tid];
       lds_sync();
@@ -1431,11 +1488,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           for (int m = M0; m < M1; ++m) {
             h[m - M0] = 0.0;
 #pragma unroll
-            for (int n = 0; n < NU; ++n) h[m - M0] += Acol[n] * S.Y[n * NU + m];
+            for (int n = 0; n < NU; ++n) h[m - M0] += Acol[n] * S.sl.Y[n * NU + m];
           }
 #pragma unroll
           for (int m = M0; m < M1; ++m)
-            S.M[c * NU + m] = (a0 * S.W[r0 * NU + m] + a1 * S.W[r1 * NU + m]) + 0.5 * h[m - M0];
+            S.sl.M[c * NU + m] = (a0 * S.W[r0 * NU + m] + a1 * S.W[r1 * NU + m]) + 0.5 * h[m - M0];
         };
         if (wv == 0)
           mcols(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
@@ -1458,7 +1515,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // the same (last) pass (spare_entry), so the passes need no divergent
         // branch and can interleave
         {
-          const int r = (qrc[k] >> 8) & 255, c = qrc[k] & 255;
+          const int r = (qrc[k] >> 27) & 31, c = (qrc[k] >> 22) & 31;
           double lv;
           if (r < NX)
             lv = S.R[rec_off_Lxx(NX) + r * NX + c];
@@ -1477,17 +1534,13 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           double h1 = 0.0, h2 = 0.0;
 #pragma unroll
           for (int m = 0; m < NU; ++m) {
-            h1 += S.M[r * NU + m] * Ar[ic * 7 + m];
-            h2 += S.M[c * NU + m] * Ar[ir * 7 + m];
+            h1 += S.sl.M[r * NU + m] * Ar[ic * 7 + m];
+            h2 += S.sl.M[c * NU + m] * Ar[ir * 7 + m];
           }
           double v = lv + g + (sc * h1 + sr * h2);
           if (r == c && r >= NX) v += preg;
-          S.Q[r * ND + c] = v;
-          S.Q[c * ND + r] = v;
-          if (c >= NX) {
-            S.H[(r - NX) * NU + (c - NX)] = v;
-            S.H[(c - NX) * NU + (r - NX)] = v;
-          }
+          S.QQ[(qrc[k] >> 11) & 2047] = v;
+          S.QQ[qrc[k] & 2047] = v;
         }
       }
       lds_sync();
@@ -1500,7 +1553,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (wv == 0) {
         double hrow[NU], Lr[NU];
 #pragma unroll
-        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.H[l * NU + j] : (l == j ? 1.0 : 0.0);
+        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.QQ[QH + l * NU + j] : (l == j ? 1.0 : 0.0);
         bool ok;
         if (!use_qp) {
 #pragma unroll
@@ -1510,9 +1563,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         } else {
           const bool v = l < NU;
           const double q = v ? S.Qv[NX + l] : 0.0;
-          const double lb = v ? S.ulb[l] - S.uu[l] : 0.0;
-          const double ub = v ? S.uub[l] - S.uu[l] : 0.0;
-          double x = v ? S.kp[l] : 0.0;
+          const double lb = v ? S.ulb[l % NU] - S.uu[l % NU] : 0.0;
+          const double ub = v ? S.uub[l % NU] - S.uu[l % NU] : 0.0;
+          double x = v ? S.kp[l % NU] : 0.0;
           int clm = 0;
           ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l);
           if (ok && v) {
@@ -1525,7 +1578,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (ok && l < NU)
 #pragma unroll
           for (int j = 0; j < NU; ++j)
-            if (j <= l) S.L[tri(l, j)] = Lr[j];
+            if (j <= l) S.sl.L[tri(l, j)] = Lr[j];
         if (l == 0) S.flag = ok ? 1 : 0;
       } else {
         if (t > 0) {
@@ -1542,7 +1595,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // clamped set is empty (always for LLT); otherwise phase E runs.
         double hrow[NU], Lr[NU];
 #pragma unroll
-        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.H[l * NU + j] : (l == j ? 1.0 : 0.0);
+        for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.QQ[QH + l * NU + j] : (l == j ? 1.0 : 0.0);
 #pragma unroll
         for (int j = 0; j < NU; ++j) Lr[j] = use_qp ? hrow[j] + (l == j ? C.qp_reg : 0.0) : hrow[j];
         const bool ok1 = chol_rows(Lr, l);
@@ -1550,7 +1603,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           if (l < NU)
 #pragma unroll
             for (int j = 0; j < NU; ++j)
-              if (j <= l) S.L1[tri(l, j)] = Lr[j];
+              if (j <= l) S.sl.L1[tri(l, j)] = Lr[j];
           // lanes of this wave read the rows the others just wrote: LDS
           // accesses of one wave complete in order; the fence keeps the
           // compiler from moving the reads above the writes
@@ -1560,17 +1613,17 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
             double col[NU];
             if (l < NX) {
 #pragma unroll
-              for (int c = 0; c < NU; ++c) col[c] = S.Q[l * ND + NX + c];
+              for (int c = 0; c < NU; ++c) col[c] = S.QQ[QXU + l * NU + c];
             } else {
 #pragma unroll
               for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
             }
-            chol_solve<NU>(S.L1, col);
+            chol_solve<NU>(S.sl.L1, col);
             if (l < NX) {
               double* Kt = K_i + (unsigned)(t * NU * NX);
 #pragma unroll
               for (int c = 0; c < NU; ++c) {
-                S.K[c * NX + l] = col[c];
+                S.sl.K[c * NX + l] = col[c];
                 Kt[c * NX + l] = col[c];
               }
             } else {
@@ -1602,17 +1655,17 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         double col[NU];
         if (l < NX) {
 #pragma unroll
-          for (int c = 0; c < NU; ++c) col[c] = S.clamped[c] ? 0.0 : S.Q[l * ND + NX + c];
+          for (int c = 0; c < NU; ++c) col[c] = S.clamped[c] ? 0.0 : S.QQ[QXU + l * NU + c];
         } else {
 #pragma unroll
           for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
         }
-        chol_solve<NU>(S.L, col);
+        chol_solve<NU>(S.sl.L, col);
         if (l < NX) {
           double* Kt = K_i + (unsigned)(t * NU * NX);
 #pragma unroll
           for (int c = 0; c < NU; ++c) {
-            S.K[c * NX + l] = col[c];
+            S.sl.K[c * NX + l] = col[c];
             Kt[c * NX + l] = col[c];
           }
         } else {
@@ -1631,10 +1684,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         double a1 = 0.0, a2 = 0.0;
 #pragma unroll
         for (int c = 0; c < NU; ++c) {
-          a1 += S.Q[i * ND + NX + c] * S.K[c * NX + j];
-          a2 += S.Q[j * ND + NX + c] * S.K[c * NX + i];
+          a1 += S.QQ[QXU + i * NU + c] * S.sl.K[c * NX + j];
+          a2 += S.QQ[QXU + j * NU + c] * S.sl.K[c * NX + i];
         }
-        const double v = S.Q[i * ND + j] - 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
+        const double v = S.QQ[i * NX + j] - 0.5 * (a1 + a2) + (i == j ? preg : 0.0);
         S.V[i * NX + j] = v;
         S.V[j * NX + i] = v;
         badv |= bad(fabs(v)) ? 1 : 0;
