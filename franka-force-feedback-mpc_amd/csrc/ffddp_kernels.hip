@@ -58,6 +58,9 @@ constexpr int NODE_GPB = NODE_BLOCK / NODE_GROUP;
 #ifndef QC_UNROLL
 #define QC_UNROLL 1
 #endif
+#ifndef QC_FF_LATE
+#define QC_FF_LATE 0  // phase C unroll of FF's latency variant (0: full; FF B=1024 +1.4 % over 1 since the LDS diet)
+#endif
 // BW_PF_LATE: when k_backward_w issues the loads of the next node's record:
 // at the top of the node (0), or after phase D with the record staged into
 // LDS at the end of the node (S.R is dead after phase C), so the prefetch
@@ -886,9 +889,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   S.uub[BW_DIET_SLOTS ? l % NU : l] = C.u_ub[l % NU];
   // this lane's lower-triangle entries of Q (phase C) and V (phase F), fixed for the whole pass
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 63) / 64;
-  // phase C unroll: full in the classical latency variant; FF's 7 passes
-  // unrolled spill into AGPRs (1.5 % slower at B=1024), so not there
-  constexpr int QC_N = LATE ? (FF ? 1 : NQL) : QC_UNROLL;
+  // phase C unroll: full in the latency variants (FF's 7 passes move into
+  // AGPRs, but since the LDS diet that is 1.4 % faster at B=1024)
+  constexpr int QC_N = LATE ? (FF ? (QC_FF_LATE ? QC_FF_LATE : NQL) : NQL) : QC_UNROLL;
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 63) / 64;
   int qrc[NQL], vij[NVL];
 #pragma unroll
