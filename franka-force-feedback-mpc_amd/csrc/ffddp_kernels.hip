@@ -2437,6 +2437,10 @@ struct ffddp_handle {
   int bw_w2_max = -1;    // ... and the two-wave variant (FFDDP_BW_W2_MAX; -1: SIMDs / (2 slices); 0: never)
   int n_simd = 1024;     // SIMDs of the device (4 per CU)
   bool fw_fill = true;   // widen the first line-search pass to fill the SIMDs (FFDDP_FW_FILL=0: off)
+  // horizon from which an 8-wide first pass takes all ten (FFDDP_FW_LONG;
+  // 0: never, the default since round 5: C5 tracking 64.0k-64.8k -> 65.7k-66.1k,
+  // random x0 29.3k -> 28.9k; round 3 measured +4.5 % for it)
+  int fw_long = 0;
   int fw_wide_max = -1;  // active instances per slice up to which the first pass takes every step length
                          // (decided on the device; FFDDP_FW_WIDE_MAX; -1: SIMDs / slices; 0: never)
   int ls_row_max = -1;   // trial groups of a line-search pass up to which it runs one group per DPP row
@@ -2678,11 +2682,11 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
         // the first pass as one wave per SIMD holds (8 groups per wave), so
         // the second pass (a whole extra rollout on the chain) is rarely needed
         if (h->fw_fill) n1 = std::max(n1, std::min(NTRIALS, 8 * h->n_simd / std::max(B, 1)));
-        // long horizons: a second pass is a rollout ~N node-calcs long, so
-        // once the first pass is 8 wide it takes all ten (N=100 point3d,
-        // B=1024: +4.5 %; at N=30 the two extra trials cost more than the
-        // rare second pass saves)
-        if (h->fw_fill && N >= 60 && n1 >= 8) n1 = NTRIALS;
+        // long horizons (FFDDP_FW_LONG, off by default): a second pass is a
+        // rollout ~N node-calcs long, so once the first pass is 8 wide it
+        // could take all ten (N=100 point3d, B=1024: +4.5 % in round 3; on
+        // the round-5 kernels -2.3 % in the tracking regime, +1.4 % random)
+        if (h->fw_fill && h->fw_long > 0 && N >= h->fw_long && n1 >= 8) n1 = NTRIALS;
         // device-side widening of the first pass: while a slice's active
         // instances fit one wave per SIMD share at every step length, all ten
         // run at once (random x0 at B=1024: the second pass ran in every
@@ -2914,6 +2918,7 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
     if (const char* bl = std::getenv("FFDDP_BW_LATE_MAX")) h->bw_late_max = std::atoi(bl);
     if (const char* bw2 = std::getenv("FFDDP_BW_W2_MAX")) h->bw_w2_max = std::atoi(bw2);
     if (const char* ff = std::getenv("FFDDP_FW_FILL")) h->fw_fill = std::atoi(ff) != 0;
+    if (const char* fl = std::getenv("FFDDP_FW_LONG")) h->fw_long = std::atoi(fl);
     if (const char* fwm = std::getenv("FFDDP_FW_WIDE_MAX")) h->fw_wide_max = std::atoi(fwm);
     if (const char* lrm = std::getenv("FFDDP_LS_ROW_MAX")) h->ls_row_max = std::atoi(lrm);
     if (const char* fsch = std::getenv("FFDDP_FW_SCHED")) {
