@@ -692,26 +692,34 @@ __device__ __forceinline__ double rowb(double v, int k) {
 }
 
 // In-place LLT of the SPD matrix whose row i is held by lane i: on exit
-// a[j] (j < i) = L_ij and a[i] = 1 / L_ii (same operation order as
-// chol_packed).  Returns false (uniformly) if a pivot is not positive.  The
-// pivot test is one ballot after the factorisation, not a branch per pivot:
-// past a bad pivot the values are garbage (NaN) but unused, and a good
-// factorisation takes the same operations either way.
+// a[j] (j < i) = L_ij and a[i] = 1 / L_ii.  Returns false (uniformly) if a
+// pivot is not positive.  The pivot test is one ballot after the
+// factorisation, not a branch per pivot: past a bad pivot the values are
+// garbage (NaN) but unused, and a good factorisation takes the same
+// operations either way.  Every product-sum is an explicit fma (and the
+// reciprocal square root's Newton steps too), so the larger basic block
+// cannot change how the compiler contracts them: every backward variant and
+// BoxQP's refactorisations round alike (wave 1's speculative factor in
+// k_backward_w2 must equal BoxQP's for an empty clamped set, bit for bit).
 __device__ __forceinline__ bool chol_rows(double (&a)[NU], int lane) {
+  bool bad = false;
 #pragma unroll
   for (int k = 0; k < NU; ++k) {
     double d = a[k];
 #pragma unroll
-    for (int m = 0; m < k; ++m) d -= a[m] * a[m];
+    for (int m = 0; m < k; ++m) d = __builtin_fma(-a[m], a[m], d);
     const double dk = rowb(d, k);
-    if (__ballot(!(dk > 0.0)) & 1ull) return false;  // lane 0 holds row 0's pivot
-    const double il = rsqrt_nr(dk);
+    bad = bad || !(dk > 0.0);  // dk is uniform across the row
+    double il = __builtin_amdgcn_rsq(dk);
+    const double h = 0.5 * dk;
+    il = il * __builtin_fma(-(h * il), il, 1.5);
+    il = il * __builtin_fma(-(h * il), il, 1.5);
     double s = a[k];
 #pragma unroll
-    for (int m = 0; m < k; ++m) s -= a[m] * rowb(a[m], k);
+    for (int m = 0; m < k; ++m) s = __builtin_fma(-a[m], rowb(a[m], k), s);
     a[k] = (lane == k) ? il : ((lane > k) ? s * il : a[k]);
   }
-  return true;
+  return !(__ballot(bad) & 1ull);  // lane 0 holds row 0's pivots
 }
 
 // solve L L^T x = r with L held as rows (chol_rows layout); r / result per lane
