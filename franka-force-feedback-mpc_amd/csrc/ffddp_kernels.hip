@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
   double hv = J ? x0[(long)b * nx + 7 + ji] : 0.0;
   double ht = (FF && J) ? x0[(long)b * nx + 14 + ji] : 0.0;
   double cost = 0.0, dvp = 0.0;
-  bool fail = false;
+  bool fail = false, fail_l = false;
   double* xtr = d.xs_try + ((long)b * NTRIALS + tr) * (N + 1) * nx;
   double* utr = d.us_try + ((long)b * NTRIALS + tr) * N * NU;
   // node inputs of the rollout, prefetched one node ahead (joint lane ji)
@@ -2005,12 +2005,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
         }
       }
       cost += g8_sum(c);
-      int brk = (bad(cost) || g8_or((J && (bad(fabs(qn)) || bad(fabs(vn)) || (FF && bad(fabs(tn))))) ? 1 : 0)) ? 1 : 0;
-      if (ROW) brk = ls_row_bcast0(brk);  // the phantom group follows the real one
-      if (brk) {
-        fail = true;
-        break;
-      }
+      // a non-finite or huge state or cost fails the trial (forwardPass's
+      // raiseIfNaN); the test is lane-local here and reduced once after the
+      // last node, so no cross-lane reduction or branch sits on each node's
+      // chain.  A failed trial's remaining nodes run on garbage whose results
+      // nothing reads (its cost and trajectory are never accepted), and a bad
+      // cost stays bad to the end
+      fail_l = fail_l || (J && (bad(fabs(qn)) || bad(fabs(vn)) || (FF && bad(fabs(tn)))));
       hq = qn;
       hv = vn;
       ht = tn;
@@ -2029,8 +2030,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
         c = fma(0.5 * C.w_y, fma(K.wy2t * e3, e3, fma(K.wy2v * e2, e2, (K.wy2q * e1) * e1)), c);
       }
       cost += g8_sum(c);
-      if (bad(cost)) fail = true;
     }
+  }
+  {
+    int f = (bad(cost) || g8_or(fail_l ? 1 : 0)) ? 1 : 0;
+    if (ROW) f = ls_row_bcast0(f);  // the phantom group follows the real one
+    fail = f != 0;
   }
   PP(9);
   PP_FLUSH_AT(16);
