@@ -778,6 +778,10 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
 #pragma unroll
     for (int j = 0; j < NU; ++j) hx += hrow[j] * xb[j];
     const double g = q + hx;
+    // the objective at x: needed only if this iteration steps, but computed
+    // here it overlaps the factorisation and solve instead of following them
+    // (a cross-lane sum cannot move across the convergence branch by itself)
+    const double fold = g8_sum(0.5 * x * hx + q * x);
     const bool c = (x == lb && g > 0.0) || (x == ub && g < 0.0);
     const bool changed = !have || ((__ballot(c != cl) & 0x7Full) != 0);
     cl = c;
@@ -799,7 +803,6 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
     }
     const double dx = cl ? 0.0 : xsf - x;
     if (lane0(max8(fabs(dx)) < C.qp_th_grad)) break;
-    const double fold = g8_sum(0.5 * x * hx + q * x);
     bool moved = false;
 #pragma unroll 1
     for (int ia = 0; ia < NTRIALS; ++ia) {
@@ -1472,10 +1475,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (tid < NU) S.z[tid] = dt2 * S.Vx[tid] + dt * S.Vx[7 + tid];
       lds_sync();
       PP(1);
-      if (t < N - 1 && (S.badw[0] | S.badw[1])) {  // node t+1's phases F / G
-        failed = true;
-        break;
-      }
+      // node t+1's phase F / G flags: read now, tested after phase B (whose
+      // results a failed pass discards), so the LDS round trip is not on the
+      // node's chain
+      const int badprev = t < N - 1 ? (S.badw[0] | S.badw[1]) : 0;
       // ---- phase B: row c of M = I~'W + 1/2 A^'Y (columns m split over the
       // two waves) ; Qv[c] = [Lx; Lu] + I~'Vx + A^'z (wave 1) ----
       if (l < ND) {
@@ -1518,6 +1521,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
       }
       lds_sync();
+      if (badprev) {
+        failed = true;
+        break;
+      }
       PP(2);
       // ---- phase C: Q lower triangle (mirrored), entries over 128 lanes ----
 #pragma unroll
