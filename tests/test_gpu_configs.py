@@ -123,9 +123,13 @@ def test_c5_per_gpu_shape_point3d_n100(monkeypatch):
         idx = picks[i0:i0 + 8]
         small.solve(_sub(batch, idx), maxiter=10)
         for j, i in enumerate(idx):
-            for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred", "stats"):
+            for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred"):
                 a, b = getattr(big, name)[i], getattr(small, name)[j]
                 assert np.array_equal(a, b, equal_nan=True), (name, int(i))
+            # the counters, except [5..7] (which line-search pass evaluated a
+            # trial depends on the batch's first-pass width, not on the instance)
+            keep = [c for c in range(big.stats.shape[1]) if c not in (5, 6, 7)]
+            assert np.array_equal(big.stats[i, keep], small.stats[j, keep]), ("stats", int(i))
     sel = picks[::2]
     from oracle import fddp
 
