@@ -1885,6 +1885,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
   if (ROW) lane_consts_fill_phantom(C, LKs, (int)threadIdx.x);
   __syncthreads();
   const LaneK& K = LKs[ROW ? (threadIdx.x & 15) : li];
+  const unsigned fl = ls_flags(C);
   const ActiveList al = active_list(d, cur);
   if (slot >= al.n) return;
   const int b = al.list[slot];
@@ -1985,7 +1986,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
           acc = fma(-pK[7 + m], dvm, acc);
           if (FF) acc = fma(-pK[14 + m], ls_get<ROW>(dtt, m), acc);
         }
-        if (C.use_box) acc = fmin(fmax(acc, K.ulb), K.uub);
+        if (fl & RF_BOX) acc = fmin(fmax(acc, K.ulb), K.uub);
         u = acc;
         if (Js) utr[(long)t * NU + ji] = u;
       }
@@ -1993,7 +1994,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
       double qn, vn, cp, lam[3];
       const double uin = FF ? xt_t : u;
       PP(8);
-      ls_node_calc<NC, ROW>(C, K, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam
+      ls_node_calc<NC, ROW>(C, fl, K, MODE_RUNNING, surf, xq_t, xv_t, uin, xq, xv, tref, ref, qn, vn, cp, lam
 #ifdef FFDDP_PHASE_PROF
                             , pp_acc, pp_last
 #endif
@@ -2026,7 +2027,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
       double qn, vn, cp, lam[3];
       const int mode = FF ? MODE_TERMINAL_U : MODE_TERMINAL_X;
       PP(8);
-      ls_node_calc<NC, ROW>(C, K, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam
+      ls_node_calc<NC, ROW>(C, fl, K, mode, surf, xq_t, xv_t, FF ? xt_t : 0.0, xq, xv, tref, ref, qn, vn, cp, lam
 #ifdef FFDDP_PHASE_PROF
                             , pp_acc, pp_last
 #endif

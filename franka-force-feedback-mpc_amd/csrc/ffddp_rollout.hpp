@@ -35,6 +35,43 @@
 
 namespace ffddp {
 
+// ---- the rollout's cost flags ----
+// Read from DevConsts inside the node loop, each flag was re-loaded by a
+// scalar load right before its branch (the scalar registers cannot hold every
+// DevConsts value the loop reads) and waited for at once.  As one bit mask
+// held in a scalar register for the whole kernel the branches need no load
+// (9 fewer scalar-memory waits per node; line search at C5 -0.6 %).  The
+// weights stay in DevConsts: staged in LDS they were hoisted out of the node
+// loop into ~80 held registers (270 -> 356 per lane, so the wave no longer
+// shares its SIMD with another stream's node or backward wave: B = 4096
+// -3.5 %; still 314 when re-read per node).
+enum : unsigned {
+  RF_STATE = 1u,    // state regularisation (classical, or FF's inner_state_reg)
+  RF_QSOFT = 2u,    // q soft limits
+  RF_TAU = 4u,      // torque regularisation (classical, or FF's inner_tau_reg)
+  RF_TSOFT = 8u,    // torque soft limits
+  RF_PZ = 16u,      // plane-z cost in contact
+  RF_VZ = 32u,      // normal-velocity cost in contact
+  RF_FC = 64u,      // friction cone
+  RF_UNI = 128u,    // unilateral force barrier
+  RF_FN = 256u,     // normal-force tracking
+  RF_BOX = 512u,    // control box clamp
+};
+__device__ __forceinline__ unsigned ls_flags(const DevConsts& C) {
+  unsigned f = 0;
+  f |= (C.variant == FFDDP_CLASSICAL || C.inner_state_reg) ? RF_STATE : 0u;
+  f |= C.has_qsoft ? RF_QSOFT : 0u;
+  f |= (C.variant == FFDDP_CLASSICAL || C.inner_tau_reg) ? RF_TAU : 0u;
+  f |= C.has_tsoft ? RF_TSOFT : 0u;
+  f |= C.has_pz ? RF_PZ : 0u;
+  f |= C.has_vz ? RF_VZ : 0u;
+  f |= C.has_fc ? RF_FC : 0u;
+  f |= C.has_uni ? RF_UNI : 0u;
+  f |= C.has_fn ? RF_FN : 0u;
+  f |= C.use_box ? RF_BOX : 0u;
+  asm volatile("" : "+s"(f));  // a register value from here on, not a re-loadable one
+  return f;
+}
 // ---- scalar helpers, explicit fma ----
 __device__ __forceinline__ double ls_dot3(double a0, double b0, double a1, double b1, double a2, double b2) {
   return fma(a2, b2, fma(a1, b1, a0 * b0));
@@ -203,14 +240,13 @@ template <bool ROW> __device__ __forceinline__ double ls_bwd(const double (&Lt)[
 // DifferentialActionModelContactFwdDynamics by its Schur complement; one
 // backward substitution instead of two full solves).
 template <int NC, bool ROW>
-__device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K, int mode, bool surface, double q,
+__device__ __forceinline__ void ls_node_calc(const DevConsts& C, unsigned fl, const LaneK& K, int mode, bool surface, double q,
                                              double v, double u, double xq, double xv, double tr, const double* ref,
                                              double& qn, double& vn, double& cpart, double (&lam)[3]
 #ifdef FFDDP_PHASE_PROF
                                              , unsigned long long (&pp_acc)[12], unsigned long long& pp_last
 #endif
 ) {
-  const ffddp_robot& rb = C.rb;
   const int li = g8_lane();
   const bool J = li < NQ;
   const bool with_dyn = mode != MODE_TERMINAL_X;
@@ -342,25 +378,25 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K,
         C.w_ee_pos * (0.5 * ls_dot3(C.ee_pos_w[0] * rx, rx, C.ee_pos_w[1] * ry, ry, C.ee_pos_w[2] * rz, rz));
     const double vx = vp[0] - ref[3], vy = vp[1] - ref[4];
     double ccon = fma(C.w_tv, 0.5 * fma(vy, vy, vx * vx), C.w_tp * (0.5 * fma(ry, ry, rx * rx)));
-    if (C.has_pz) {
+    if (fl & RF_PZ) {
       const double pz = pee[2] - (ref[2] - C.z_press);
       ccon = fma(C.w_pz, 0.5 * (pz * pz), ccon);
     }
-    if (C.has_vz) ccon = fma(C.w_vz, 0.5 * (vp[2] * vp[2]), ccon);
+    if (fl & RF_VZ) ccon = fma(C.w_vz, 0.5 * (vp[2] * vp[2]), ccon);
     cee += surface ? ccon : cfree;
   }
   double cj = 0.0;  // this joint's state / control costs
   if (J) {
-    if (C.variant == FFDDP_CLASSICAL || C.inner_state_reg) {
+    if (fl & RF_STATE) {
       const double rq = q - xq, rv = v - xv;
       cj = C.w_post * (0.5 * fma(rv, rv, rq * rq));
       cj = fma(C.w_v, 0.5 * ((K.vdw * v) * v), cj);
     }
-    if (C.has_qsoft) cj = fma(C.w_qs, ls_barrier(q - K.qsx, K.qslb, K.qsub), cj);
-    if (!terminal && (C.variant == FFDDP_CLASSICAL || C.inner_tau_reg)) {
+    if (fl & RF_QSOFT) cj = fma(C.w_qs, ls_barrier(q - K.qsx, K.qslb, K.qsub), cj);
+    if (!terminal && (fl & RF_TAU)) {
       const double r = u - tr;
       cj = fma(C.w_tau, 0.5 * (r * r), cj);
-      if (C.has_tsoft) cj = fma(C.w_ts, ls_barrier(u, K.tslb, K.tsub), cj);
+      if (fl & RF_TSOFT) cj = fma(C.w_ts, ls_barrier(u, K.tslb, K.tsub), cj);
     }
   }
   lam[0] = lam[1] = lam[2] = 0.0;
@@ -407,7 +443,7 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K,
       for (int k = 0; k < 3; ++k) ha[k] = t1[k] + Iww[k];
       ls_cross(cw, al, t1);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) f1[k] = m * ((aO[k] - rb.gravity[k]) - t1[k]);
+      for (int k = 0; k < 3; ++k) f1[k] = m * ((aO[k] - C.rb.gravity[k]) - t1[k]);
       ls_cross(cw, f1, t1);
 #pragma unroll
       for (int k = 0; k < 3; ++k) n1[k] = t1[k] + Ial[k];
@@ -578,12 +614,12 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, const LaneK& K,
     if (mode != MODE_TERMINAL_X)
 #pragma unroll
       for (int r = 0; r < NC; ++r) lm[r] = lam[r];
-    if (NC == 3 && C.has_fc) cf += ls_friction_cone(C, lm);
-    if (C.has_uni) {
+    if (NC == 3 && (fl & RF_FC)) cf += ls_friction_cone(C, lm);
+    if (fl & RF_UNI) {
 #pragma unroll
       for (int r = 0; r < NC; ++r) cf = fma(C.w_uni, ls_barrier(lm[r], C.uni_lb[r], C.uni_ub[r]), cf);
     }
-    if (C.has_fn) {
+    if (fl & RF_FN) {
 #pragma unroll
       for (int r = 0; r < NC; ++r) {
         const double e = lm[r] - C.fn_ref[r];
