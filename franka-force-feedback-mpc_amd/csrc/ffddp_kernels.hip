@@ -396,6 +396,19 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
     const double sc = scale ? C.dt : 1.0;
     const double* D = P.D;
     const double* g = P.g;
+    // FF's y-cost weights of this lane's components, loaded once up front:
+    // at each use the scalar w_y and the lane's Wy2 entry were loaded again
+    // and waited for with vmcnt(0), i.e. behind every record store in flight
+    // (FF k_node 109 -> 104 us at B = 1024; the compiler contracts some of
+    // the products differently, so FF solves move by <= 2e-9, classical
+    // ones are bit-identical)
+    double wy = 0.0, wy2j = 0.0, wy2u = 0.0;
+    if (ff) {
+      wy = C.w_y;
+      wy2j = C.Wy2[lane < 14 ? lane : 0];
+      wy2u = C.Wy2[14 + (lane < 7 ? lane : 0)];
+      asm volatile("" : "+s"(wy), "+v"(wy2j), "+v"(wy2u));
+    }
     if (lane < 14) {
       const int j = lane;
       // dynamics Jacobian columns
@@ -409,14 +422,14 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
         acc += fquad<NC>(&G.col[i][12], D + 12, P.Dfo, col + 12);
         if (i == j) acc += P.Dx[j];
         acc *= sc;
-        if (ff && i == j) acc += C.w_y * C.Wy2[j];
+        if (ff && i == j) acc += wy * wy2j;
         Lxx[i * nx + j] = acc;
       }
       // Lx_in[j]
       double lx = 0.0;
       for (int r = 0; r < nd; ++r) lx += col[r] * g[r];
       lx = (lx + P.gx[j]) * sc;
-      if (ff) lx += C.w_y * C.Wy2[j] * (y[j] - x0[(long)b * nx + j]);
+      if (ff) lx += wy * wy2j * (y[j] - x0[(long)b * nx + j]);
       rec[rec_off_Lx(nx) + j] = lx;
       // Lxu_in row j (force rows only): classical -> Lxu row j; FF -> Lxx_aug[14+k][j]
       if (need_u) {
@@ -456,8 +469,8 @@ __global__ __launch_bounds__(NODE_BLOCK) __attribute__((amdgpu_waves_per_eu(NODE
           Lxx[i * nx + 14 + kk] = acc * sc;
         }
         for (int m = 0; m < NU; ++m)
-          Lxx[(14 + m) * nx + 14 + kk] = luu[m] + (m == kk ? C.w_y * C.Wy2[14 + kk] : 0.0);
-        rec[rec_off_Lx(nx) + 14 + kk] = lu + C.w_y * C.Wy2[14 + kk] * (y[14 + kk] - x0[(long)b * nx + 14 + kk]);
+          Lxx[(14 + m) * nx + 14 + kk] = luu[m] + (m == kk ? wy * wy2u : 0.0);
+        rec[rec_off_Lx(nx) + 14 + kk] = lu + wy * wy2u * (y[14 + kk] - x0[(long)b * nx + 14 + kk]);
         // augmented control terms: Lu = w_w w + w_s g_soft ; Luu = diag ; Lxu = 0
         double wk = 0.0;
         if (!terminal) wk = usrc[(long)t * NU + kk];

@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU tests on the in-tree library; bit comparison against lib/head (the
+# previous commit's build); FF and classical A/B head vs main; then the
+# stagger / caller-slice knobs (tools/ab_ff_knobs_r05.sh).
+set -e
+R=${GRAFT_REPO_ROOT:-/root/repo}
+TAG=${1:-r05g}
+O=$R/gpurun_out/$TAG; mkdir -p $O
+cd $R
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+FFDDP_LIB=$R/franka-force-feedback-mpc_amd/lib/head/libffddp.so timeout -k 10 200 python3 tools/lib_dump.py $O/a.npz > $O/dump_a.log 2>&1
+timeout -k 10 200 python3 tools/lib_dump.py $O/b.npz > $O/dump_b.log 2>&1
+python3 tools/lib_dump.py --compare $O/a.npz $O/b.npz | tee $O/bits.txt; rm -f $O/a.npz $O/b.npz
+BATCHES="1024 4096" BENCH_ARGS="--variant ff" bash tools/ab_libs.sh $TAG/ff head main main head
+BATCHES="4096" bash tools/ab_libs.sh $TAG/cls head main
+echo "step ab done"
+bash tools/ab_ff_knobs_r05.sh $TAG/knob
+echo "step knob done"
