@@ -245,12 +245,21 @@ __device__ __forceinline__ void primal_group(const DevConsts& C, const Dev& d, c
   const double q = y[ji], v = y[7 + ji];
   const double u = (uin != nullptr) ? uin[ji] : 0.0;
   // setCandidate: the accepted line-search trial becomes (xs, us) here, node
-  // by node, instead of a whole-trajectory copy on the iteration's chain
-  const double* xdst = d.xs + (long)b * (N + 1) * nx;
-  if (J && xsrc != xdst) {
+  // by node, instead of a whole-trajectory copy on the iteration's chain.
+  // Classical: stored at the end of the calc from registers; issued here,
+  // the stores sat in front of the vmcnt(0) wait of every later load (the
+  // per-lane cost constants in node_primal_g8, the gaps' next state).  FF
+  // (at its register limit: the late stores spill) stores here.
+  const bool commit = J && xsrc != d.xs + (long)b * (N + 1) * nx;
+  double cu = 0.0;
+  if (commit) {
+    if (FF) {
 #pragma unroll
-    for (int k = 0; k < (FF ? 3 : 2); ++k) d.xs[((long)b * (N + 1) + t) * nx + 7 * k + li] = y[7 * k + li];
-    if (!terminal) d.us[((long)b * N + t) * NU + li] = usrc[(long)t * NU + li];
+      for (int k = 0; k < 3; ++k) d.xs[((long)b * (N + 1) + t) * nx + 7 * k + li] = y[7 * k + li];
+      if (!terminal) d.us[((long)b * N + t) * NU + li] = usrc[(long)t * NU + li];
+    } else if (!terminal) {
+      cu = usrc[(long)t * NU + li];
+    }
   }
   double lam[3];
   const double pc = node_primal_g8<NC>(C, mode, surf, q, v, u, xreg[ji], xreg[7 + ji], xreg[14 + ji], ref,
@@ -306,7 +315,14 @@ __device__ __forceinline__ void primal_group(const DevConsts& C, const Dev& d, c
 #pragma unroll
       for (int k = 0; k < (FF ? 3 : 2); ++k) f[7 * k + li] = feas ? 0.0 : x0[(long)b * nx + 7 * k + li] - y[7 * k + li];
     }
-  }}
+  }
+  if (!FF && commit) {
+    double* xr = d.xs + ((long)b * (N + 1) + t) * nx;
+    xr[li] = q;
+    xr[7 + li] = v;
+    if (!terminal) d.us[((long)b * N + t) * NU + li] = cu;
+  }
+}
 
 // a^T H b over the contact-force block of the Gauss-Newton Hessian: diagonal
 // Dd plus (nc = 3) the friction cone's off-diagonal couplings Do
