@@ -32,11 +32,15 @@ Prints ONE JSON line (rank 0).  Extra objects:
                 and horizon, with its own roofline.
   host_io       PCIe-inclusive rate of the host-array entry point.
 roofline.fp64 prices the same run against the measured fp64 VALU peak
-(tools/micro/fp64_peak.hip -> profiles/r05_fp64_peak.json): issued fp64
-lane-flops per node stage / backward node / trial node from a PMC pass of
-this configuration (tools/pmc_fp64.sh -> profiles/fp64_latest.json) x the
-device-counted units of this run.  roofline.bound names the roof the run is
-closer to; roofline.frac stays SURVEY §8(d)'s HBM fraction.
+(tools/micro/fp64_peak.hip -> profiles/r05_fp64_peak.json) with the USEFUL
+flops: the operation count of the scalar C++ implementation per node stage /
+backward node / trial node (tools/flop_count.py -> profiles/
+r06_useful_flops.json) x the device-counted units of this run.  Its
+issue_rate field is the issued fp64 lane-flops of a PMC pass of this
+configuration (tools/pmc_fp64.sh -> profiles/fp64_latest.json: every lane of
+every issued wave instruction, idle lanes included) on the same roof.
+roofline.bound names the roof the run is closer to by the useful figure;
+roofline.frac stays SURVEY §8(d)'s HBM fraction.
 """
 from __future__ import annotations
 
@@ -173,6 +177,28 @@ def solve_counts(stats: np.ndarray) -> dict:
             "trials": float((s[:, 6] + s[:, 7]).sum()), "forward_launches": float(s[:, 5].sum())}
 
 
+def useful_per_unit(variant, contact, N):
+    """Useful (algorithmic) fp64 flops per node stage / backward node / trial
+    node of this OCP: the scalar C++ CPU baseline executed with a counting
+    fp64 type (tools/flop_count.py -> profiles/r06_useful_flops.json; no SIMD
+    lanes, so no idle or duplicate lanes), if the file holds this config."""
+    f = ROOT / "profiles" / "r06_useful_flops.json"
+    try:
+        c = json.loads(f.read_text())["configs"][f"{variant}/{contact}/N{N}"]
+        return {k: c["phases"][k]["flops_per_unit"] for k in ("node", "backward", "forward")}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def useful_flops(stats, N, per) -> float | None:
+    """Useful fp64 flops of one batched solve: useful_per_unit x this solve's
+    device-counted units."""
+    if not per:
+        return None
+    u = solve_units(stats, N)
+    return sum(per[c] * u[c] for c in ("node", "backward", "forward"))
+
+
 def fp64_flops(stats, N, per_unit) -> float | None:
     """Issued fp64 lane-flops of one batched solve: the PMC per-unit figures
     (tools/pmc_fp64.py) x this solve's device-counted units."""
@@ -200,6 +226,29 @@ def rooflines(bytes_per_step, flops_per_step, sec_per_step, world):
         fp = {"achieved": flops_per_step / sec_per_step / 1e12, "peak": pk * world, "unit": "TFLOP/s"}
         fp["frac"] = fp["achieved"] / fp["peak"]
     return hbm, fp
+
+
+def fp64_block(fp, useful_flops_step, per_unit, fpi, issued_flops_step):
+    """roofline.fp64: the useful-work fraction (frac; algorithmic flops of the
+    scalar implementation per unit x device-counted units / time / measured
+    fp64 FMA peak) and, beside it, the issue-rate utilisation (issued fp64
+    lane-flops from the PMC: every lane of every issued wave instruction,
+    idle and duplicate lanes included)."""
+    if fp is None and fpi is None:
+        return None
+    out = {} if fp is None else dict(fp, useful=True, flops_per_step=useful_flops_step, flops_per_unit=per_unit,
+                                     basis="useful fp64 flops per node stage / backward node / trial node of the "
+                                           "scalar C++ implementation (oracle/cpu/ffddp_cpu.cpp run with a counting "
+                                           "fp64 type, tools/flop_count.py -> profiles/r06_useful_flops.json) x this "
+                                           "run's device-counted units, over the measured fp64 FMA peak "
+                                           "(tools/micro/fp64_peak.hip, profiles/r05_fp64_peak.json)")
+    if fpi is not None:
+        out["issue_rate"] = dict(fpi, flops_per_step=issued_flops_step, basis=(
+            "issue-rate utilisation: issued fp64 lane-flops (64 x (2 FMA + MUL + ADD) per wave instruction, every "
+            "lane, masked ones included; tools/pmc_fp64.sh, profiles/fp64_latest.json) x device-counted units"))
+        if fp is not None and fpi["achieved"] > 0:
+            out["useful_share_of_issued"] = fp["achieved"] / fpi["achieved"]
+    return out
 
 
 def cpu_baseline(cfg, batch, maxiter: int, budget_s: float) -> dict:
@@ -349,11 +398,15 @@ def main():
     sb = solve_bytes(stats, nx, nu, N)
     fp_unit = _profile_json("fp64_latest.json", args.variant, args.contact, B, N)
     fl = fp64_flops(stats, N, fp_unit)
-    # whole-job sums over ranks: algorithmic bytes per step, ok count, iterations, fp64 flops
+    uf_unit = useful_per_unit(args.variant, args.contact, N)
+    ufl = useful_flops(stats, N, uf_unit)
+    # whole-job sums over ranks: algorithmic bytes per step, ok count, iterations, fp64 flops (issued, useful)
     tot = shard.sum_over_ranks(torch.tensor([sb["total"], sb["total_survey_formula"], float(ok.sum()),
-                                             float(iters.sum()), fl if fl is not None else -1.0], **f64)).cpu().numpy()
-    tot_bytes, tot_survey, tot_ok, tot_it, tot_fl = (float(v) for v in tot)
+                                             float(iters.sum()), fl if fl is not None else -1.0,
+                                             ufl if ufl is not None else -1.0], **f64)).cpu().numpy()
+    tot_bytes, tot_survey, tot_ok, tot_it, tot_fl, tot_ufl = (float(v) for v in tot)
     tot_fl = tot_fl if fl is not None else None
+    tot_ufl = tot_ufl if ufl is not None else None
     unit_counts = {k: float(v) for k, v in zip(("calcdiff", "backward", "trials", "forward_launches"),
                                            shard.sum_over_ranks(torch.tensor(list(solve_counts(stats).values()),
                                                                              **f64)).cpu().numpy())}
@@ -403,8 +456,13 @@ def main():
             pu = (fp_unit or {}).get("kernels", {}).get("forward" if k == "forward2" else k, {})
             if pk64 and "lane_flops_per_unit" in pu and k in pun:
                 fpl = pu["lane_flops_per_unit"] * pun[k] * n_prof / n
-                e.update({"fp64_flops_per_launch": fpl,
-                          "fp64_frac": fpl / (ms / n / 1e3) / 1e12 / pk64})
+                e.update({"fp64_issued_flops_per_launch": fpl,
+                          "fp64_issue_frac": fpl / (ms / n / 1e3) / 1e12 / pk64})
+            uk = "forward" if k == "forward2" else k
+            if pk64 and uf_unit and uk in uf_unit and k in pun:
+                ufl_k = uf_unit[uk] * pun[k] * n_prof / n
+                e.update({"fp64_useful_flops_per_launch": ufl_k,
+                          "fp64_useful_frac": ufl_k / (ms / n / 1e3) / 1e12 / pk64})
             kernels[k] = e
         dom = max((k for k in kernels if "achieved_gbs" in kernels[k]), key=lambda k: kernels[k]["ms_per_solve"])
         dominant = dict(name=dom, **kernels[dom])
@@ -413,17 +471,18 @@ def main():
         if args.profile_only:
             if rank == 0:
                 print(json.dumps({"profile_only": True, "kernels": kernels, "dominant": dominant}), flush=True)
-            if dist.is_initialized():
-                dist.destroy_process_group()
+            shard.shutdown()
             return
 
     value = B * world * args.steps / elapsed
     traffic = pmc_traffic(args.variant, args.contact, B, N) if world == 1 else None
-    hbm, fp = rooflines(tot_bytes, tot_fl, elapsed / args.steps, world)
+    hbm, fp = rooflines(tot_bytes, tot_ufl, elapsed / args.steps, world)
+    _, fpi = rooflines(tot_bytes, tot_fl, elapsed / args.steps, world)
     roofline = {
         # the roof this run is closer to: SURVEY §8(d)'s HBM roof, or the
-        # measured fp64 VALU roof that the kernels' issued work is priced
-        # against (the counters show them chain- and issue-bound)
+        # measured fp64 VALU roof priced with the USEFUL flops (the scalar
+        # algorithm's operation count; the issued lane-flops, idle lanes
+        # included, are reported as issue-rate utilisation beside it)
         "bound": "fp64_valu" if fp is not None and fp["frac"] > hbm["frac"] else "hbm",
         "scope": "whole solve: algorithmic bytes of every kernel (SURVEY.md §8(d) per-node words x device-counted "
                  "calcDiffs / backward passes / line-search launches and step lengths, all ranks) / wall time "
@@ -436,10 +495,7 @@ def main():
         "bytes_per_step": tot_bytes,
         "frac_survey_formula": tot_survey * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world),
         "frac_of_measured_copy": tot_bytes * args.steps / elapsed / 1e9 / (HBM_MEASURED_GBS * world),
-        "fp64": None if fp is None else dict(fp, flops_per_step=tot_fl, basis=(
-            "issued fp64 lane-flops (64 x (2 FMA + MUL + ADD) per wave instruction, per node stage / backward node "
-            "/ trial node from tools/pmc_fp64.sh, profiles/fp64_latest.json) x this run's device-counted units, "
-            "over the measured fp64 FMA peak (tools/micro/fp64_peak.hip, profiles/r05_fp64_peak.json)")),
+        "fp64": fp64_block(fp, tot_ufl, uf_unit, fpi, tot_fl),
         "dominant_kernel": dominant,
         # what the SQ counters of this configuration show limits the kernels
         # (profiles/sq_latest.json, when it is for this configuration)
@@ -462,10 +518,15 @@ def main():
         rit = float(shard.sum_over_ranks(torch.tensor([float(TR["iters"].sum().item())], **f64)).cpu()[0])
         rstats = TR["stats"].cpu().numpy()
         rby = float(shard.sum_over_ranks(torch.tensor([solve_bytes(rstats, nx, nu, N)["total"]], **f64)).cpu()[0])
-        rh, _ = rooflines(rby, None, el / rs, world)
+        rufl = useful_flops(rstats, N, uf_unit)
+        if rufl is not None:
+            rufl = float(shard.sum_over_ranks(torch.tensor([rufl], **f64)).cpu()[0])
+        rh, rfp = rooflines(rby, rufl, el / rs, world)
         extras["random_regime"] = {"value": B * world * rs / el, "unit": "solves/s", "ms_per_step": el / rs * 1e3,
                                    "scaling": "weak", "ok_frac": rok / (B * world), "mean_iter": rit / (B * world),
-                                   "roofline": dict(rh, bound="hbm", bytes_per_step=rby)}
+                                   "roofline": dict(rh, bound="fp64_valu" if rfp and rfp["frac"] > rh["frac"] else "hbm",
+                                                    bytes_per_step=rby,
+                                                    fp64=fp64_block(rfp, rufl, uf_unit, None, None))}
         del TR
         if world > 1:
             # strong scaling: rank 0's B-instance batch split into contiguous
@@ -519,13 +580,19 @@ def main():
             ffl = fp64_flops(fst, N, _profile_json("fp64_latest_ff.json", "ff", args.contact, B, N))
             if ffl is not None:
                 ffl = float(shard.sum_over_ranks(torch.tensor([ffl], **f64)).cpu()[0])
-            fh, ffp = rooflines(fby, ffl, el / fs_, world)
+            fuf_unit = useful_per_unit("ff", args.contact, N)
+            fufl = useful_flops(fst, N, fuf_unit)
+            if fufl is not None:
+                fufl = float(shard.sum_over_ranks(torch.tensor([fufl], **f64)).cpu()[0])
+            fh, ffpu = rooflines(fby, fufl, el / fs_, world)
+            _, ffpi = rooflines(fby, ffl, el / fs_, world)
+            ffp = fp64_block(ffpu, fufl, fuf_unit, ffpi, ffl)
             extras["ff"] = {"value": B * world * fs_ / el, "unit": "solves/s", "ms_per_step": el / fs_ * 1e3,
                             "scaling": "weak", "workload": f"ForceFeedback (q,v,tau_hat)/w nx=21 nu=7, horizon={N}, "
                                                           f"batch={B} per GPU, maxiter={args.maxiter}, "
                                                           f"contact={args.contact}",
                             "ok_frac": fok / (B * world), "mean_iter": fit / (B * world),
-                            "roofline": dict(fh, bound="fp64_valu" if ffp and ffp["frac"] > fh["frac"] else "hbm",
+                            "roofline": dict(fh, bound="fp64_valu" if ffp and ffp.get("frac", 0) > fh["frac"] else "hbm",
                                              bytes_per_step=fby, fp64=ffp)}
             fsolver.close()
             del TF
@@ -609,8 +676,7 @@ def main():
             **extras,
         }
         print(json.dumps(line), flush=True)
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    shard.shutdown()  # the reserved handle, then the process group
 
 
 if __name__ == "__main__":

@@ -636,8 +636,10 @@ __device__ __forceinline__ int spare_entry(int e, int nqe, int last) {
 // phase C's packed entry (r >= c): r, c and the two flat BwW::QQ indices its
 // value is stored at (Qxx mirrored; Qux stored once as Qxu[c][r - NX]; Quu
 // mirrored into H)
-template <int NX> __device__ __forceinline__ int q_entry(int r, int c) {
-  int i1, i2;
+template <int NX> __device__ __forceinline__ unsigned q_entry(int r, int c) {
+  // fields: r, c 5 bits each, i1, i2 11 bits each
+  static_assert(NX + NU <= 32 && (NX + NU) * (NX + NU) <= 2048, "q_entry packing");
+  unsigned i1, i2;
   if (r < NX) {
     i1 = r * NX + c;
     i2 = c * NX + r;
@@ -647,7 +649,7 @@ template <int NX> __device__ __forceinline__ int q_entry(int r, int c) {
     i1 = NX * NX + NX * NU + (r - NX) * NU + (c - NX);
     i2 = NX * NX + NX * NU + (c - NX) * NU + (r - NX);
   }
-  return (r << 27) | (c << 22) | (i1 << 11) | i2;
+  return ((unsigned)r << 27) | ((unsigned)c << 22) | (i1 << 11) | i2;
 }
 
 // nonzeros of column c of I~ (the Euler identity part of [Fx Fu]):
@@ -933,7 +935,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
   // AGPRs, but since the LDS diet that is 1.4 % faster at B=1024)
   constexpr int QC_N = LATE ? (FF ? (QC_FF_LATE ? QC_FF_LATE : NQL) : NQL) : QC_UNROLL;
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 63) / 64;
-  int qrc[NQL], vij[NVL];
+  unsigned qrc[NQL];
+  int vij[NVL];
 #pragma unroll
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
@@ -1354,7 +1357,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // this lane's lower-triangle entries of Q (phase C) and V (phase F) over 128 lanes
   constexpr int NQE = ND * (ND + 1) / 2, NQL = (NQE + 127) / 128;
   constexpr int NVE = NX * (NX + 1) / 2, NVL = (NVE + 127) / 128;
-  int qrc[NQL], vij[NVL];
+  unsigned qrc[NQL];
+  int vij[NVL];
 #pragma unroll
   for (int k = 0; k < NQL; ++k) {
     int r = 0, c = 0;
@@ -3125,6 +3129,9 @@ int ffddp_solve_batch_dev(ffddp_handle* h, int B, const double* x0, const double
   if (!x0 || !node_ref || !inst_ref || !surface || !xs_init || !us_init || !xs || !us || !K || !cost || !iters || !ok)
     return fail(h, FFDDP_E_INVALID, "null pointer");
   HIPCHK(h, hipSetDevice(h->device));
+  // the handle's workspace is shared by every solve: a solve enqueued on
+  // another (possibly non-blocking) stream must finish before this one starts
+  if (h->last_done_set) HIPCHK(h, hipStreamWaitEvent((hipStream_t)stream, h->last_done, 0));
   const int rc = launch_solve(h, B, x0, node_ref, inst_ref, surface, xs_init, us_init, maxiter, is_feasible, xs, us,
                               K, cost, iters, ok, fn_pred, stats, (hipStream_t)stream);
   if (rc) return rc;
@@ -3211,6 +3218,12 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
   // would be a fifth stream on the process's 4 hardware queues and share one
   // with a slice (measured: 15.3 vs 11.6 ms per B = 4096 solve)
   hipStream_t cs = nullptr;
+  // after an asynchronous device-entry solve still running on a caller
+  // stream (possibly non-blocking): this solve reuses its workspace
+  if (h->last_done_set) {
+    const hipError_t e = hipStreamWaitEvent(cs, h->last_done, 0);
+    if (e != hipSuccess) return fail(h, FFDDP_E_DEVICE, std::string("hipStreamWaitEvent: ") + hipGetErrorString(e));
+  }
   int rc = launch_solve(h, B, h->in_x0, h->in_nref, h->in_iref, h->in_surf, h->in_xs, h->in_us, maxiter, is_feasible,
                         (double*)hout[0], (double*)hout[1], (double*)hout[2], h->out_cost, h->out_iters, h->out_ok,
                         h->out_fn, h->out_stats, cs, &io);

@@ -198,10 +198,17 @@ def _quat_wxyz_to_R(q) -> np.ndarray:
 class _MPCBase:
     variant = "classical"
 
-    def __init__(self, sim, traj_fn: Traj, config, device: int = 0, use_plan: bool = True):
+    def __init__(self, sim, traj_fn: Traj, config, device: int = 0, use_plan: bool = True, calibration_obs=None):
         """use_plan: run each tick's solve through a captured solve plan
         (BatchedBoxFDDP.plan: one graph launch per tick, bit-identical to
-        solve()); False: the plain host-array solve."""
+        solve()); False: the plain host-array solve.
+        calibration_obs: the observation the site calibration
+        (_calibrate_site_rotation / _calibrate_site_position_offset) is taken
+        from; default the sim's initial observation, as the reference does
+        (crocoddyl_classical.py:199-226).  The calibration is a rigid offset,
+        so another posture changes it at rounding level only; the fleet
+        controller calibrates once for all its instances, and its tick-for-tick
+        comparisons pass the fleet's observation here."""
         cfg = config
         self.sim = sim
         self.traj_fn = traj_fn
@@ -213,8 +220,9 @@ class _MPCBase:
         self.nx_mb = 14
         obs0 = sim.get_observation(with_ee=True, with_jacobian=False)
         self.q_nom = np.asarray(obs0.q, dtype=float).copy()
-        self.R_site_from_pin_ee = self._calibrate_site_rotation(obs0)
-        self.p_site_minus_frame_pin = self._calibrate_site_position_offset(obs0)
+        obs_cal = obs0 if calibration_obs is None else calibration_obs
+        self.R_site_from_pin_ee = self._calibrate_site_rotation(obs_cal)
+        self.p_site_minus_frame_pin = self._calibrate_site_position_offset(obs_cal)
         self.R_des = self._rot_mj_to_pin(R.vertical_down_rotation_mj())
         self.xs: Optional[List[np.ndarray]] = None
         self.us: Optional[List[np.ndarray]] = None
@@ -443,8 +451,9 @@ class ClassicalCrocoddylMPC(_MPCBase):
     variant = "classical"
 
     def __init__(self, sim, traj_fn: Traj, config: Optional[ClassicalMPCConfig] = None, device: int = 0,
-                 use_plan: bool = True):
-        super().__init__(sim, traj_fn, config if config is not None else ClassicalMPCConfig(), device, use_plan)
+                 use_plan: bool = True, calibration_obs=None):
+        super().__init__(sim, traj_fn, config if config is not None else ClassicalMPCConfig(), device, use_plan,
+                         calibration_obs)
 
     def _initial_tau(self, obs0):
         return obs0.tau_bias

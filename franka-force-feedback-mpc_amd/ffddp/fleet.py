@@ -189,7 +189,10 @@ class FleetClassicalMPC:
         # _policy_control (:759-779): u = us[0] + s K[0] (x - xs[0])
         tau_raw = np.where(self.valid[:, None], us0, self.tau_prev)
         if cfg.use_feedback_policy:
-            fb = float(cfg.feedback_gain_scale) * np.einsum("bij,bj->bi", K0, x0 - xs0)
+            # stacked matmul: per instance the same gemv as the scalar
+            # controller's K[0] @ dx (np.einsum sums in another order and
+            # differs in the last bit for about half the entries)
+            fb = float(cfg.feedback_gain_scale) * np.matmul(K0, (x0 - xs0)[:, :, None])[:, :, 0]
             tau_raw = np.where(self.valid[:, None], tau_raw + fb, tau_raw)
         policy_idx = np.where(self.valid, 0, -1)
         tau_raw_inf = np.max(np.abs(tau_raw), 1)
@@ -348,7 +351,7 @@ def run_sweep(scenarios: Sequence[str] = ("flat", "tilted_5", "tilted_10", "tilt
                instances=B, shard=(lo, hi), n_all=n_all)
     if rec_idx:
         out["record"] = dict(index=np.array(rec_idx), t=rec_t, obs=rec_obs, tau=rec_tau, q0=q0[rec_idx], traj=traj,
-                             config=cfg, dt=plant.dt)
+                             config=cfg, dt=plant.dt, calibration_obs=obs0)
     return out
 
 

@@ -54,6 +54,16 @@ def prepare_device(local_rank: int):
         _RESERVED.append(BatchedBoxFDDP(classical_preset(2, "normal_1d"), max_batch=1, device=local_rank))
 
 
+def shutdown():
+    """Close the handle prepare_device reserved (and with it the slice
+    streams' last reference) and then the process group, so neither outlives
+    the HIP runtime or RCCL at interpreter teardown.  Idempotent."""
+    while _RESERVED:
+        _RESERVED.pop().close()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def init(backend: str, local_rank: int, world: int, force: bool = False):
     """Process group for world > 1 (MASTER_ADDR defaults to 127.0.0.1).
     force: a one-process group as well (an in-memory store), so that one GPU

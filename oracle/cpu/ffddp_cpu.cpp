@@ -35,6 +35,16 @@ constexpr int NXMAX = 21;
 
 inline bool bad(double v) { return std::isnan(v) || std::isinf(v) || v >= 1e30; }
 
+// phase / unit hooks for tools/flops/flop_count.cpp (the fp64 operation
+// count of this scalar solver per node stage, backward node and trial node);
+// no-ops in the baseline build
+#ifndef FFDDP_CPU_PHASE_SCOPE
+#define FFDDP_CPU_PHASE_SCOPE(p)
+#endif
+#ifndef FFDDP_CPU_UNIT
+#define FFDDP_CPU_UNIT(p) ((void)0)
+#endif
+
 // crocoddyl::BoxQP::solve (projected Newton, oracle/fddp.py:boxqp): the free
 // sub-problem is solved on the full 7x7 matrix with clamped rows/columns
 // replaced by identity rows; refactored whenever the free set changes.
@@ -149,6 +159,7 @@ struct Inst {
 // cost (IAM scaling and FF augmentation included).
 template <int NC, bool FF>
 double node_diff(const DevConsts& C, Inst& I, int t, double* r, double* xnext) {
+  FFDDP_CPU_UNIT(1);
   const int N = I.N;
   constexpr int nx = FF ? 21 : 14;
   constexpr int nc = NC;
@@ -282,6 +293,7 @@ double node_diff(const DevConsts& C, Inst& I, int t, double* r, double* xnext) {
 // ShootingProblem::calcDiff + the FDDP gaps (SolverFDDP::calcDiff)
 template <int NC, bool FF>
 void calc_diff(const DevConsts& C, Inst& I) {
+  FFDDP_CPU_PHASE_SCOPE(1);
   const int N = I.N, nx = I.nx;
   double c = 0.0;
   for (int t = 0; t <= N; ++t) {
@@ -321,6 +333,7 @@ void dynamics_jacobians(const DevConsts& C, const Inst& I, const double* r, doub
 
 // SolverDDP::backwardPass + SolverBoxFDDP::computeGains; false = backward failure
 bool backward(const DevConsts& C, Inst& I) {
+  FFDDP_CPU_PHASE_SCOPE(2);
   const int N = I.N, nx = I.nx;
   const double preg = I.preg;
   const bool use_qp = C.use_box && I.feas;
@@ -344,6 +357,7 @@ bool backward(const DevConsts& C, Inst& I) {
   double Fx[NXMAX * NXMAX], Fu[NXMAX * NU], FxTV[NXMAX * NXMAX], FuTV[NU * NXMAX];
   double Qxx[NXMAX * NXMAX], Qxu[NXMAX * NU], Qx[NXMAX];
   for (int t = N - 1; t >= 0; --t) {
+    FFDDP_CPU_UNIT(2);
     const double* r = I.recs.data() + (size_t)t * I.rec;
     const double* Vp = I.Vxx.data() + (size_t)(t + 1) * nx * nx;
     const double* vp = I.Vx.data() + (size_t)(t + 1) * nx;
@@ -470,6 +484,7 @@ bool backward(const DevConsts& C, Inst& I) {
 // expected improvement
 template <int NC, bool FF>
 double forward(const DevConsts& C, Inst& I, double alpha, double* dv) {
+  FFDDP_CPU_PHASE_SCOPE(3);
   const int N = I.N, nx = I.nx;
   const bool gap = !(I.feas || alpha == 1.0);
   double xh[NXMAX];
@@ -477,6 +492,7 @@ double forward(const DevConsts& C, Inst& I, double alpha, double* dv) {
   double cost = 0.0, dvv = 0.0;
   Primal P;
   for (int t = 0; t <= N; ++t) {
+    FFDDP_CPU_UNIT(3);
     const double* xs_t = I.xs.data() + (size_t)t * nx;
     const double* fs_t = I.fs.data() + (size_t)t * nx;
     double* xt = I.xs_try.data() + (size_t)t * nx;

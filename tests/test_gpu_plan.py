@@ -118,3 +118,48 @@ def test_plan_lifetime_rules():
         plan.run()
     plan.close()  # idempotent
     ref.close()
+
+
+def test_host_and_device_solves_after_side_stream_solve():
+    """the host entry point (caller slice on the null stream) and
+    a device solve on a second non-blocking stream both reuse the workspace of
+    a device solve still running on a non-blocking side stream; each waits for
+    it on the device.  Results equal fresh handles' bit for bit."""
+    import torch
+
+    N, B = 30, 300  # several slices: the slice streams fork from the caller's stream
+    cfg = product_cfg("classical", N)
+    dev = torch.device("cuda", 0)
+    f64 = dict(dtype=torch.float64, device=dev)
+
+    def dev_inputs(b):
+        return dict(x0=torch.tensor(b.x0, **f64), node_ref=torch.tensor(b.node_ref, **f64),
+                    inst_ref=torch.tensor(b.inst_ref, **f64),
+                    surface=torch.tensor(b.surface, dtype=torch.uint8, device=dev),
+                    xs_init=torch.tensor(b.xs_init, **f64), us_init=torch.tensor(b.us_init, **f64),
+                    xs=torch.zeros((B, N + 1, 14), **f64), us=torch.zeros((B, N, 7), **f64),
+                    K=torch.zeros((B, N, 7, 14), **f64), cost=torch.zeros(B, **f64),
+                    iters=torch.zeros(B, dtype=torch.int32, device=dev),
+                    ok=torch.zeros(B, dtype=torch.uint8, device=dev), fn_pred=torch.zeros((B, 2), **f64),
+                    stats=torch.zeros((B, _abi.NSTATS), dtype=torch.int32, device=dev))
+
+    b1 = make_batch("classical", B, N, seed=21, regime="random")  # long solves: still running when the next is enqueued
+    b2 = make_batch("classical", B, N, seed=22)
+    b3 = make_batch("classical", B, N, seed=23, surface=0)
+    s = BatchedBoxFDDP(cfg, max_batch=B)
+    t1, t3 = dev_inputs(b1), dev_inputs(b3)
+    side1, side2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    s.solve_dev(t1, maxiter=10, stream=side1.cuda_stream)
+    s.solve(b2, maxiter=10)  # host entry point right behind it
+    host = {k: np.copy(getattr(s, k)) for k in ("xs", "us", "K", "cost", "iter", "stats")}
+    s.solve_dev(t1, maxiter=10, stream=side1.cuda_stream)
+    s.solve_dev(t3, maxiter=10, stream=side2.cuda_stream)  # another non-blocking stream
+    torch.cuda.synchronize(dev)
+    for b, got in ((b1, {k: t1[k].cpu().numpy() for k in ("xs", "us", "K", "cost", "stats")}), (b2, host),
+                   (b3, {k: t3[k].cpu().numpy() for k in ("xs", "us", "K", "cost", "stats")})):
+        ref = BatchedBoxFDDP(cfg, max_batch=B)
+        ref.solve(b, maxiter=10)
+        for k, v in got.items():
+            assert np.array_equal(v, getattr(ref, k), equal_nan=True), k
+        ref.close()
+    s.close()

@@ -70,7 +70,7 @@ def _worker(rank, world, port, q):
         tot = shard.sum_over_ranks(torch.tensor([float(b1 - b0)])).item()
         q.put((r, (b0, b1), out, elapsed, tot))
     finally:
-        dist.destroy_process_group()
+        shard.shutdown()
 
 
 def test_two_rank_strong_split_and_gathers():
@@ -143,9 +143,11 @@ def _forced_worker(q):
         out = g(local)
         # the collective ran (the gather went through the process group's
         # buffers, not the one-process shortcut) and kept the rows
-        q.put((bool(torch.equal(out, local)), bool(torch.equal(g.recv[0], local))))
+        res = (bool(torch.equal(out, local)), bool(torch.equal(g.recv[0], local)))
     finally:
-        dist.destroy_process_group()
+        shard.shutdown()  # bench's exit path: the process group goes (idempotent)
+    shard.shutdown()
+    q.put(res + (not dist.is_initialized(),))
 
 
 def test_forced_one_process_group():
@@ -155,4 +157,4 @@ def test_forced_one_process_group():
     p.start()
     p.join(120)
     assert p.exitcode == 0
-    assert q.get(timeout=5) == (True, True)
+    assert q.get(timeout=5) == (True, True, True)

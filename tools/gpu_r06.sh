@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-6 GPU steps named in $STEPS, each under its own time limit, stopping
+# at the first failure.  Steps not listed here are tools/gpu_r05.sh's.
+#   hostio   host entry point timeline at B=4096: stage-in / enqueue / per-slice done and
+#            copied times (FFDDP_HOSTIO_TIMING), pageable and page-locked outputs (tools/hostio.py)
+#   avail    the SQ counters this box's rocprofv3 exposes (lane-utilisation candidates)
+#   lanes    VALU lane utilisation per kernel class (tools/pmc_lanes.sh)
+# usage: [STEPS="bits tests hostio"] tools/gpu_r06.sh TAG
+set -e
+R=${GRAFT_REPO_ROOT:-/root/repo}
+TAG=${1:-r06}
+O=$R/gpurun_out/$TAG; mkdir -p $O
+cd $R
+STEPS=${STEPS:-"tests bench"}
+for st in $STEPS; do
+  case $st in
+    hostio) HOSTIO_CONFIGS=${HOSTIO_CONFIGS:-pageable:0,pinned:0} timeout -k 10 200 python3 tools/hostio.py 4096 ${HOSTIO_REPS:-5} \
+              > $O/hostio.txt 2>&1 || { tail -20 $O/hostio.txt; exit 1; }
+            grep -v amdgpu.ids $O/hostio.txt | tail -14 | cut -c1-400 ;;
+    avail) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --list-avail > $O/avail.txt 2>&1) || { tail -5 $O/avail.txt; exit 1; }
+           grep -o -E "SQ_[A-Z0-9_]*(THREAD|LANE|ACTIVE|VALU)[A-Z0-9_]*" $O/avail.txt | sort -u | tr '\n' ' '; echo ;;
+    lanes) BENCH_ARGS="${LANE_ARGS:---batch 4096}" bash $R/tools/pmc_lanes.sh $TAG/lanes > $O/lanes.log 2>&1 || { tail -20 $O/lanes.log; exit 1; }
+           cat $O/lanes.log ;;
+    *) STEPS=$st bash $R/tools/gpu_r05.sh $TAG ;;
+  esac
+  echo "step $st done"
+done
