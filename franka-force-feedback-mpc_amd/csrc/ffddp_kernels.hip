@@ -22,6 +22,7 @@
 //               next k_node reads it and writes it into xs / us; k_commit at
 //               the end of the solve for the rest).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <cmath>
 #include <cstdio>
@@ -31,6 +32,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -1986,6 +1989,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
   };
   fetch(0);
   for (int t = 0; t <= N; ++t) {
+    // the lane predicates, recomputed per node from an opaque lane index
+    // (kept across the loop they are scalar-register masks that spill;
+    // ffddp_rollout.hpp FFDDP_LS_OPAQUE_LANE)
+#if FFDDP_LS_OPAQUE_LANE
+    int lt = (int)threadIdx.x;
+    asm volatile("" : "+v"(lt));
+    const bool J = (lt & (G8 - 1)) < NQ;
+    const bool Js = J && (!ROW || (lt & 8) == 0);
+#endif
     double xq_t = hq, xv_t = hv, xt_t = ht;
     const double sq = pxs[0], sv = pxs[1], stt = pxs[2];
     if (gap) {
@@ -2432,6 +2444,108 @@ struct HostIO {
   // filled by launch_solve_t: the slices [b0[k], b0[k] + bk[k])
   int ns = 0;
   int b0[8] = {0}, bk[8] = {0};
+  // optional: called before slice k's input copies are enqueued (the host
+  // stages that slice's pageable inputs); with it the slices are enqueued
+  // one after the other instead of iteration by iteration
+  std::function<int(int)> stage;
+  // optional: xs / us / K are not copied down by launch_solve_t and done[k]
+  // is not recorded there (the caller enqueues both later on ss[k], from the
+  // slice's device buffers dxs / dus / dK)
+  bool defer_out = false;
+  hipStream_t ss[8] = {};
+  const double *dxs[8] = {}, *dus[8] = {}, *dK[8] = {};
+};
+
+// Host memcpy / zero-fill pool of the host entry point: persistent threads
+// (FFDDP_COPY_THREADS, default the CPUs this process may use, at most 16)
+// that split a list of jobs into 1 MiB pieces with the calling thread.
+struct CopyJob {
+  void* dst;
+  const void* src;  // nullptr: zero-fill dst (first touch of fresh output pages)
+  size_t n;
+};
+class CopyPool {
+ public:
+  explicit CopyPool(int nthreads) {
+    for (int i = 1; i < nthreads; ++i) th_.emplace_back([this] { worker(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread& t : th_) t.join();
+  }
+  int threads() const { return (int)th_.size() + 1; }
+  void run(const std::vector<CopyJob>& jobs) {
+    constexpr size_t kPiece = size_t(1) << 20;
+    std::vector<CopyJob> pieces;
+    size_t tot = 0;
+    for (const CopyJob& j : jobs) {
+      for (size_t o = 0; o < j.n; o += kPiece)
+        pieces.push_back(CopyJob{(char*)j.dst + o, j.src ? (const char*)j.src + o : nullptr, std::min(kPiece, j.n - o)});
+      tot += j.n;
+    }
+    if (pieces.empty()) return;
+    if (th_.empty() || tot < 4 * kPiece) {  // small: the calling thread alone
+      for (const CopyJob& c : pieces) exec(c);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      work_ = &pieces;
+      next_.store(0);
+      left_ = pieces.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return left_ == 0; });
+    work_ = nullptr;
+  }
+
+ private:
+  static void exec(const CopyJob& c) {
+    if (c.src)
+      std::memcpy(c.dst, c.src, c.n);
+    else
+      std::memset(c.dst, 0, c.n);
+  }
+  void drain() {
+    size_t did = 0;
+    const std::vector<CopyJob>* w = work_;
+    for (size_t i = next_++; i < w->size(); i = next_++) {
+      exec((*w)[i]);
+      ++did;
+    }
+    if (did) {
+      std::lock_guard<std::mutex> lk(mu_);
+      left_ -= did;
+      if (left_ == 0) done_cv_.notify_all();
+    }
+  }
+  void worker() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && work_ != nullptr); });
+        if (stop_) return;
+        seen = gen_;
+      }
+      drain();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::vector<CopyJob>* work_ = nullptr;
+  std::atomic<size_t> next_{0};
+  size_t left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
 };
 
 struct ffddp_handle {
@@ -2453,6 +2567,7 @@ struct ffddp_handle {
   char* stage = nullptr;
   size_t stage_bytes = 0;
   std::vector<hipEvent_t> hdone;
+  CopyPool* pool = nullptr;  // host copies of the host entry point (first host solve)
   // per-iteration trace (ffddp_trace_enable)
   double* trace = nullptr;
   int trace_it = 0;
@@ -2659,139 +2774,143 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
       io->b0[k] = sl[k].b0;
       io->bk[k] = sl[k].B;
     }
-    // host entry point: each slice's inputs go up on its own stream, so slice
-    // k's copies overlap slice k-1's kernels
-    for (int k = 0; k < S; ++k)
-      for (int i = 0; i < io->n_in; ++i) {
-        const size_t o = (size_t)sl[k].b0 * io->in[i].per_inst;
-        HIPCHK(h, hipMemcpyAsync((char*)io->in[i].dev + o, (const char*)io->in[i].host + o,
-                                 (size_t)sl[k].B * io->in[i].per_inst, hipMemcpyHostToDevice, sl[k].s));
-      }
   }
-  for (int k = 0; k < S; ++k) {
+  // host entry point: slice k's inputs go up on its own stream, so its
+  // copies overlap the other slices' kernels
+  auto enqueue_in = [&](int k) -> int {
+    for (int i = 0; i < io->n_in; ++i) {
+      const size_t o = (size_t)sl[k].b0 * io->in[i].per_inst;
+      HIPCHK(h, hipMemcpyAsync((char*)io->in[i].dev + o, (const char*)io->in[i].host + o,
+                               (size_t)sl[k].B * io->in[i].per_inst, hipMemcpyHostToDevice, sl[k].s));
+    }
+    return 0;
+  };
+  auto enqueue_init = [&](int k) {
     ProfScope p(h, sl[k].s, KC_INIT);
     const long b0 = sl[k].b0;
     hipLaunchKernelGGL(k_init, dim3(1024), dim3(256), 0, sl[k].s, h->dc, sl[k].d, xs_init + b0 * N1 * nxl,
                        us_init + b0 * (long)N * NU, is_feasible);
-  }
-  for (int it = 0; it < maxiter; ++it) {
-    for (int k = 0; k < S; ++k) {
-      const Dev& d = sl[k].d;
-      const hipStream_t ss = sl[k].s;
-      const int Bk = sl[k].B;
-      const long b0 = sl[k].b0;
-      const double* x0k = x0 + b0 * nxl;
-      const double* nrefk = nref + b0 * N1 * 6;
-      const double* irefk = iref + b0 * 21;
-      const uint8_t* surfk = surf + b0;
-      const long nodes = (long)Bk * (N + 1);
-      // optional start stagger: slice k's first node stage waits for slice
-      // k-1's, so the throughput-bound node stages do not all collide
-      if (it == 0 && k > 0 && stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
-      if (it == 0 && stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
-      {
-        ProfScope p(h, ss, KC_NODE);
-        hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, ss,
-                           h->dc, d, x0k, nrefk, irefk, surfk, 0, it & 1);
-      }
-      if (it == 0 && stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
-      {
-        ProfScope p(h, ss, KC_BACKWARD);
-        const int lmax = h->bw_late_max >= 0 ? h->bw_late_max : h->n_simd / S;
-        // two-wave variant: for slices no larger than one wave per SIMD share
-        // (small per-GPU batches, where the whole solve is latency-bound) at
-        // one wave per SIMD; in the tails of large slices (active count up to
-        // lmax) at two waves per SIMD, so its blocks need not wait for the
-        // other slices' kernels to free whole SIMDs (the one-wave kernel there:
-        // B = 4096 -1.7 %; this one +2 % over LATE).  FF's
-        // two-wave pass spills too much at two waves per SIMD: LATE there.
-        const bool small = Bk <= h->n_simd / S;
-        const int w2auto = small ? h->n_simd / (2 * S) : (FF ? 0 : lmax);
-        const int w2max = std::min(lmax, h->bw_w2_max >= 0 ? h->bw_w2_max : w2auto);
-        if (lmax < Bk)
-          hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1, lmax, w2max);
-        if (lmax > w2max && w2max < Bk)
-          hipLaunchKernelGGL((k_backward_w<FF, true>), dim3(lmax < Bk ? lmax : Bk), dim3(64), 0, ss, h->dc, d, it, it & 1,
-                             lmax, w2max);
-        if (w2max > 0) {
-          const dim3 g2(w2max < Bk ? w2max : Bk);
-          if constexpr (!FF) {
-            if (!small) {
-              hipLaunchKernelGGL((k_backward_w2<FF, 2>), g2, dim3(128), 0, ss, h->dc, d, it, it & 1, w2max);
-            } else {
-              hipLaunchKernelGGL((k_backward_w2<FF, 1>), g2, dim3(128), 0, ss, h->dc, d, it, it & 1, w2max);
-            }
+  };
+  // one FDDP iteration of slice k: node stage, backward pass, line search, step decision
+  auto enqueue_iter = [&](int k, int it) -> int {
+    const Dev& d = sl[k].d;
+    const hipStream_t ss = sl[k].s;
+    const int Bk = sl[k].B;
+    const long b0 = sl[k].b0;
+    const double* x0k = x0 + b0 * nxl;
+    const double* nrefk = nref + b0 * N1 * 6;
+    const double* irefk = iref + b0 * 21;
+    const uint8_t* surfk = surf + b0;
+    const long nodes = (long)Bk * (N + 1);
+    // optional start stagger: slice k's first node stage waits for slice
+    // k-1's, so the throughput-bound node stages do not all collide
+    if (it == 0 && k > 0 && stagger) HIPCHK(h, hipStreamWaitEvent(ss, h->stg[k - 1], 0));
+    if (it == 0 && stagger == 2 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
+    {
+      ProfScope p(h, ss, KC_NODE);
+      hipLaunchKernelGGL((k_node<NC, FF>), dim3((int)((nodes + NODE_GPB - 1) / NODE_GPB)), dim3(NODE_BLOCK), 0, ss,
+                         h->dc, d, x0k, nrefk, irefk, surfk, 0, it & 1);
+    }
+    if (it == 0 && stagger == 1 && k + 1 < S) HIPCHK(h, hipEventRecord(h->stg[k], ss));
+    {
+      ProfScope p(h, ss, KC_BACKWARD);
+      const int lmax = h->bw_late_max >= 0 ? h->bw_late_max : h->n_simd / S;
+      // two-wave variant: for slices no larger than one wave per SIMD share
+      // (small per-GPU batches, where the whole solve is latency-bound) at
+      // one wave per SIMD; in the tails of large slices (active count up to
+      // lmax) at two waves per SIMD, so its blocks need not wait for the
+      // other slices' kernels to free whole SIMDs (the one-wave kernel there:
+      // B = 4096 -1.7 %; this one +2 % over LATE).  FF's
+      // two-wave pass spills too much at two waves per SIMD: LATE there.
+      const bool small = Bk <= h->n_simd / S;
+      const int w2auto = small ? h->n_simd / (2 * S) : (FF ? 0 : lmax);
+      const int w2max = std::min(lmax, h->bw_w2_max >= 0 ? h->bw_w2_max : w2auto);
+      if (lmax < Bk)
+        hipLaunchKernelGGL((k_backward_w<FF>), dim3(Bk), dim3(64), 0, ss, h->dc, d, it, it & 1, lmax, w2max);
+      if (lmax > w2max && w2max < Bk)
+        hipLaunchKernelGGL((k_backward_w<FF, true>), dim3(lmax < Bk ? lmax : Bk), dim3(64), 0, ss, h->dc, d, it, it & 1,
+                           lmax, w2max);
+      if (w2max > 0) {
+        const dim3 g2(w2max < Bk ? w2max : Bk);
+        if constexpr (!FF) {
+          if (!small) {
+            hipLaunchKernelGGL((k_backward_w2<FF, 2>), g2, dim3(128), 0, ss, h->dc, d, it, it & 1, w2max);
           } else {
             hipLaunchKernelGGL((k_backward_w2<FF, 1>), g2, dim3(128), 0, ss, h->dc, d, it, it & 1, w2max);
           }
+        } else {
+          hipLaunchKernelGGL((k_backward_w2<FF, 1>), g2, dim3(128), 0, ss, h->dc, d, it, it & 1, w2max);
         }
-      }
-      int n1 = NTRIALS;
-      {
-        // first pass: trials 0..n1-1, per-iteration schedule (fw_sched) then
-        // fw_first; the second pass evaluates the rest for the instances that
-        // accepted none of them
-        n1 = it < (int)h->fw_sched.size() ? h->fw_sched[it] : h->fw_first;
-        // a small batch leaves SIMDs idle: evaluate as many step lengths in
-        // the first pass as one wave per SIMD holds (8 groups per wave), so
-        // the second pass (a whole extra rollout on the chain) is rarely needed
-        if (h->fw_fill) n1 = std::max(n1, std::min(NTRIALS, 8 * h->n_simd / std::max(B, 1)));
-        // long horizons (FFDDP_FW_LONG, off by default): a second pass is a
-        // rollout ~N node-calcs long, so once the first pass is 8 wide it
-        // could take all ten (N=100 point3d, B=1024: +4.5 % in round 3; on
-        // the round-5 kernels -2.3 % in the tracking regime, +1.4 % random)
-        if (h->fw_fill && h->fw_long > 0 && N >= h->fw_long && n1 >= 8) n1 = NTRIALS;
-        // device-side widening of the first pass: while a slice's active
-        // instances fit one wave per SIMD share at every step length, all ten
-        // run at once (random x0 at B=1024: the second pass ran in every
-        // iteration)
-        const int wide = h->fw_wide_max >= 0 ? h->fw_wide_max : h->n_simd / S;
-        const long g1 = std::max((long)Bk * n1, (long)std::min(Bk, wide) * NTRIALS);  // first-pass groups
-        // layout of each pass (ffddp_rollout.hpp): one trial group per DPP
-        // row while the pass's groups fit row_max, two otherwise, decided on
-        // the device from the active count.  Only slices that fit one wave
-        // per SIMD share take the row layout at all: a large slice's late
-        // passes would gain it, but launching both layouts every pass (the
-        // unchosen one exits at once) cost more than that at B = 4096
-        // (507.9k vs 512.4k solves/s).  When every possible
-        // pass of the slice fits, only the row layout is launched.
-        const int row_max = (h->ls_row_max >= 0 ? h->ls_row_max : 4 * h->n_simd / S) *
-                            (h->ls_row_max < 0 && Bk > h->n_simd / S ? 0 : 1);
-        const bool row_only = row_max > 0 && (long)Bk * NTRIALS <= (long)row_max;
-        auto fw = [&](int tr0, int ntr, int more) {
-          const long groups = more ? (long)Bk * ntr : g1;
-          if (!row_only) {
-            const dim3 grid((unsigned)((groups * G8 + 63) / 64));
-            hipLaunchKernelGGL((k_forward_g8<NC, FF, false>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
-                               surfk, tr0, ntr, more, it & 1, wide, row_max);
-          }
-          if (row_max > 0) {
-            const long rg = std::min(groups, (long)row_max);  // the row layout runs only when they fit
-            const dim3 grid((unsigned)((rg * 16 + 63) / 64));
-            hipLaunchKernelGGL((k_forward_g8<NC, FF, true>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
-                               surfk, tr0, ntr, more, it & 1, wide, row_max);
-          }
-        };
-        {
-          ProfScope p(h, ss, KC_FORWARD);
-          fw(0, n1, 0);
-        }
-        if (n1 < NTRIALS) {
-          ProfScope p(h, ss, KC_FORWARD2);
-          fw(n1, NTRIALS - n1, 1);
-        }
-      }
-      {
-        ProfScope p(h, ss, KC_ACCEPT);
-        hipLaunchKernelGGL(k_accept, dim3((Bk + 63) / 64), dim3(64), 0, ss, h->dc, d, it, n1, it & 1,
-                           h->fw_wide_max >= 0 ? h->fw_wide_max : h->n_simd / S);
       }
     }
-  }
+    int n1 = NTRIALS;
+    {
+      // first pass: trials 0..n1-1, per-iteration schedule (fw_sched) then
+      // fw_first; the second pass evaluates the rest for the instances that
+      // accepted none of them
+      n1 = it < (int)h->fw_sched.size() ? h->fw_sched[it] : h->fw_first;
+      // a small batch leaves SIMDs idle: evaluate as many step lengths in
+      // the first pass as one wave per SIMD holds (8 groups per wave), so
+      // the second pass (a whole extra rollout on the chain) is rarely needed
+      if (h->fw_fill) n1 = std::max(n1, std::min(NTRIALS, 8 * h->n_simd / std::max(B, 1)));
+      // long horizons (FFDDP_FW_LONG, off by default): a second pass is a
+      // rollout ~N node-calcs long, so once the first pass is 8 wide it
+      // could take all ten (N=100 point3d, B=1024: +4.5 % in round 3; on
+      // the round-5 kernels -2.3 % in the tracking regime, +1.4 % random)
+      if (h->fw_fill && h->fw_long > 0 && N >= h->fw_long && n1 >= 8) n1 = NTRIALS;
+      // device-side widening of the first pass: while a slice's active
+      // instances fit one wave per SIMD share at every step length, all ten
+      // run at once (random x0 at B=1024: the second pass ran in every
+      // iteration)
+      const int wide = h->fw_wide_max >= 0 ? h->fw_wide_max : h->n_simd / S;
+      const long g1 = std::max((long)Bk * n1, (long)std::min(Bk, wide) * NTRIALS);  // first-pass groups
+      // layout of each pass (ffddp_rollout.hpp): one trial group per DPP
+      // row while the pass's groups fit row_max, two otherwise, decided on
+      // the device from the active count.  Only slices that fit one wave
+      // per SIMD share take the row layout at all: a large slice's late
+      // passes would gain it, but launching both layouts every pass (the
+      // unchosen one exits at once) cost more than that at B = 4096
+      // (507.9k vs 512.4k solves/s).  When every possible
+      // pass of the slice fits, only the row layout is launched.
+      const int row_max = (h->ls_row_max >= 0 ? h->ls_row_max : 4 * h->n_simd / S) *
+                          (h->ls_row_max < 0 && Bk > h->n_simd / S ? 0 : 1);
+      const bool row_only = row_max > 0 && (long)Bk * NTRIALS <= (long)row_max;
+      auto fw = [&](int tr0, int ntr, int more) {
+        const long groups = more ? (long)Bk * ntr : g1;
+        if (!row_only) {
+          const dim3 grid((unsigned)((groups * G8 + 63) / 64));
+          hipLaunchKernelGGL((k_forward_g8<NC, FF, false>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
+                             surfk, tr0, ntr, more, it & 1, wide, row_max);
+        }
+        if (row_max > 0) {
+          const long rg = std::min(groups, (long)row_max);  // the row layout runs only when they fit
+          const dim3 grid((unsigned)((rg * 16 + 63) / 64));
+          hipLaunchKernelGGL((k_forward_g8<NC, FF, true>), grid, dim3(64), 0, ss, h->dc, d, x0k, nrefk, irefk,
+                             surfk, tr0, ntr, more, it & 1, wide, row_max);
+        }
+      };
+      {
+        ProfScope p(h, ss, KC_FORWARD);
+        fw(0, n1, 0);
+      }
+      if (n1 < NTRIALS) {
+        ProfScope p(h, ss, KC_FORWARD2);
+        fw(n1, NTRIALS - n1, 1);
+      }
+    }
+    {
+      ProfScope p(h, ss, KC_ACCEPT);
+      hipLaunchKernelGGL(k_accept, dim3((Bk + 63) / 64), dim3(64), 0, ss, h->dc, d, it, n1, it & 1,
+                         h->fw_wide_max >= 0 ? h->fw_wide_max : h->n_simd / S);
+    }
+    return 0;
+  };
   const size_t bxs = (size_t)(N + 1) * nx * sizeof(double);
   const size_t bus = (size_t)N * NU * sizeof(double);
   const size_t bks = (size_t)N * NU * nx * sizeof(double);
-  for (int k = 0; k < S; ++k) {
+  // the end of slice k's solve: accepted trials committed, results, and
+  // (host entry point) its outputs down and its completion event
+  auto enqueue_tail = [&](int k) -> int {
     const Dev& d = sl[k].d;
     const hipStream_t ss = sl[k].s;
     const long b0 = sl[k].b0;
@@ -2809,16 +2928,49 @@ int launch_solve_t(ffddp_handle* h, int B, const double* x0, const double* nref,
     // host entry point: page-locked host memory, the slice's results go
     // down as soon as it finishes (the device entry point solved in place)
     if (io) {
-      HIPCHK(h, hipMemcpyAsync(xs + b0 * N1 * nxl, d.xs, bxs * Bk, hipMemcpyDefault, ss));
-      HIPCHK(h, hipMemcpyAsync(us + b0 * (long)N * NU, d.us, bus * Bk, hipMemcpyDefault, ss));
-      HIPCHK(h, hipMemcpyAsync(K + b0 * (long)N * NU * nx, d.K, bks * Bk, hipMemcpyDefault, ss));
+      io->ss[k] = ss;
+      io->dxs[k] = d.xs;
+      io->dus[k] = d.us;
+      io->dK[k] = d.K;
+      if (!io->defer_out) {
+        HIPCHK(h, hipMemcpyAsync(xs + b0 * N1 * nxl, d.xs, bxs * Bk, hipMemcpyDefault, ss));
+        HIPCHK(h, hipMemcpyAsync(us + b0 * (long)N * NU, d.us, bus * Bk, hipMemcpyDefault, ss));
+        HIPCHK(h, hipMemcpyAsync(K + b0 * (long)N * NU * nx, d.K, bks * Bk, hipMemcpyDefault, ss));
+      }
       for (int i = 0; i < io->n_out; ++i) {
         const size_t o = (size_t)b0 * io->out[i].per_inst;
         HIPCHK(h, hipMemcpyAsync((char*)io->out[i].host + o, (const char*)io->out[i].dev + o,
                                  (size_t)Bk * io->out[i].per_inst, hipMemcpyDeviceToHost, ss));
       }
-      HIPCHK(h, hipEventRecord(io->done[k], ss));
+      if (!io->defer_out) HIPCHK(h, hipEventRecord(io->done[k], ss));
     }
+    return 0;
+  };
+  if (io && io->stage) {
+    // host entry point with pageable inputs: slice by slice, the host stages
+    // slice k's inputs into page-locked memory and enqueues its whole solve
+    // before staging slice k+1, so the staging of the later slices overlaps
+    // the earlier slices' copies and kernels
+    for (int k = 0; k < S; ++k) {
+      if (const int rc = io->stage(k)) return rc;
+      if (const int rc = enqueue_in(k)) return rc;
+      enqueue_init(k);
+      for (int it = 0; it < maxiter; ++it)
+        if (const int rc = enqueue_iter(k, it)) return rc;
+      if (const int rc = enqueue_tail(k)) return rc;
+    }
+  } else {
+    // iteration-major across the slices (the device entry point and solve
+    // plans; the host entry point with page-locked inputs)
+    if (io)
+      for (int k = 0; k < S; ++k)
+        if (const int rc = enqueue_in(k)) return rc;
+    for (int k = 0; k < S; ++k) enqueue_init(k);
+    for (int it = 0; it < maxiter; ++it)
+      for (int k = 0; k < S; ++k)
+        if (const int rc = enqueue_iter(k, it)) return rc;
+    for (int k = 0; k < S; ++k)
+      if (const int rc = enqueue_tail(k)) return rc;
   }
   if (hipGetLastError() != hipSuccess) return fail(h, FFDDP_E_DEVICE, "kernel launch failed");
   if (S > 1) {
@@ -2900,32 +3052,17 @@ bool host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
-// host memcpys, cut into 1 MiB pieces shared by up to 8 threads when the
-// total is large (one core moves ~10 GB/s; the staging copies of a B = 4096
-// solve are ~150 MB)
-struct CopyJob {
-  void* dst;
-  const void* src;
-  size_t n;
-};
-void host_copy(const std::vector<CopyJob>& jobs) {
-  constexpr size_t kPiece = size_t(1) << 20;
-  std::vector<CopyJob> pieces;
-  size_t tot = 0;
-  for (const CopyJob& j : jobs) {
-    for (size_t o = 0; o < j.n; o += kPiece)
-      pieces.push_back(CopyJob{(char*)j.dst + o, (const char*)j.src + o, std::min(kPiece, j.n - o)});
-    tot += j.n;
+// the host-copy pool's size: FFDDP_COPY_THREADS, else the CPUs this process
+// may run on (the GPU box grants 16 per GPU), at most 16
+int copy_threads() {
+  if (const char* e = std::getenv("FFDDP_COPY_THREADS")) {
+    const int v = std::atoi(e);
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
   }
-  const size_t nt = std::min<size_t>(8, tot / (4 * kPiece));
-  std::atomic<size_t> next{0};
-  auto work = [&] {
-    for (size_t i = next++; i < pieces.size(); i = next++) std::memcpy(pieces[i].dst, pieces[i].src, pieces[i].n);
-  };
-  std::vector<std::thread> th;
-  for (size_t i = 1; i < nt; ++i) th.emplace_back(work);
-  work();
-  for (std::thread& t : th) t.join();
+  cpu_set_t cs;
+  int n = 8;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = CPU_COUNT(&cs);
+  return n < 1 ? 1 : (n > 16 ? 16 : n);
 }
 
 bool valid_cfg(const ffddp_ocp_config& c) {
@@ -3103,6 +3240,7 @@ void ffddp_destroy(ffddp_handle* h) {
   for (hipEvent_t e : h->stg) (void)hipEventDestroy(e);
   if (!h->streams.empty()) stream_pool_release(h->device, (int)h->streams.size());
   for (hipEvent_t e : h->hdone) (void)hipEventDestroy(e);
+  delete h->pool;
   free_all(h);
   delete h;
 }
@@ -3182,26 +3320,45 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
     HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     h->hdone.push_back(e);
   }
+  if (!h->pool) h->pool = new (std::nothrow) CopyPool(copy_threads());
+  if (!h->pool) return fail(h, FFDDP_E_OOM, "copy pool");
+  CopyPool& pool = *h->pool;
   HostIO io;
   io.done = h->hdone.data();
-  // inputs: page-locked caller memory goes up directly, pageable memory
-  // through the staging buffer (one parallel host copy before the launches)
   const bool tm = std::getenv("FFDDP_HOSTIO_TIMING") != nullptr;
   auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = tm ? now() : 0.0;
+  // inputs: page-locked caller memory goes up directly, pageable memory
+  // through the staging buffer, slice by slice: the host stages slice k and
+  // enqueues its whole solve, then stages slice k+1 while slice k runs
   const void* uin[6] = {x0, node_ref, inst_ref, surface, xs_init, us_init};
   void* din[6] = {h->in_x0, h->in_nref, h->in_iref, h->in_surf, h->in_xs, h->in_us};
-  std::vector<CopyJob> jobs;
+  bool stin[6];
+  bool any_in = false;
   for (int i = 0; i < 6; ++i) {
-    const void* src = uin[i];
-    if (!host_pinned(src)) {
-      jobs.push_back(CopyJob{h->stage + off[i], src, per[i] * (size_t)B});
-      src = h->stage + off[i];
-    }
-    io.in[io.n_in++] = HostIO::In{din[i], src, per[i]};
+    stin[i] = !host_pinned(uin[i]);
+    any_in |= stin[i];
+    io.in[io.n_in++] = HostIO::In{din[i], stin[i] ? (const void*)(h->stage + off[i]) : uin[i], per[i]};
   }
-  host_copy(jobs);
-  const double t1 = tm ? now() : 0.0;
+  // FFDDP_HOSTIO_REGISTER=1: page-lock the pageable xs / us / K for the call
+  // (see below) instead of draining them through the staging buffer
+  {
+    const char* r = std::getenv("FFDDP_HOSTIO_REGISTER");
+    io.defer_out = r && std::atoi(r) != 0 && (!host_pinned(xs) || !host_pinned(us) || !host_pinned(K));
+  }
+  double tst[8] = {0};
+  if (any_in)
+    io.stage = [&](int k) {
+      std::vector<CopyJob> jobs;
+      for (int i = 0; i < 6; ++i)
+        if (stin[i]) {
+          const size_t o = (size_t)io.b0[k] * per[i];
+          jobs.push_back(CopyJob{h->stage + off[i] + o, (const char*)uin[i] + o, (size_t)io.bk[k] * per[i]});
+        }
+      pool.run(jobs);
+      if (tm) tst[k] = now();
+      return 0;
+    };
   // outputs: slice by slice into page-locked caller memory, else into the
   // staging buffer and from there into the caller's arrays as each slice ends
   void* uout[8] = {xs, us, K, cost, iters, ok, fn_pred, stats};
@@ -3229,20 +3386,79 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
                         h->out_fn, h->out_stats, cs, &io);
   if (rc) return drain_host_solve(h, rc);
   const double t2 = tm ? now() : 0.0;
+  // while the device solves: the first touch of the caller's pageable output
+  // arrays (fresh numpy arrays are unmapped pages; faulting them in during
+  // the drain below would sit on the solve's tail), by the same threads
+  {
+    std::vector<CopyJob> jobs;
+    for (int i = 0; i < 8; ++i)
+      if (staged[i]) jobs.push_back(CopyJob{uout[i], nullptr, (size_t)B * per[6 + i]});
+    pool.run(jobs);
+  }
+  // register mode: the (now resident) pageable xs / us / K are page-locked
+  // for this call and copied into by DMA directly, slice by slice (no host
+  // copy after the solve); an array the runtime will not register goes
+  // through the staging buffer as usual
+  struct Registered {
+    void* p[3] = {nullptr, nullptr, nullptr};
+    ~Registered() {
+      for (void* q : p)
+        if (q) (void)hipHostUnregister(q);
+    }
+  } regd;
+  if (io.defer_out) {
+    for (int i = 0; i < 3; ++i) {
+      if (!staged[i]) continue;
+      if (hipHostRegister(uout[i], (size_t)B * per[6 + i], hipHostRegisterDefault) == hipSuccess) {
+        regd.p[i] = uout[i];
+        staged[i] = false;  // DMA straight into the caller's array
+        hout[i] = uout[i];
+      } else {
+        (void)hipGetLastError();
+      }
+    }
+    for (int k = 0; k < io.ns; ++k) {
+      const size_t b0 = (size_t)io.b0[k], bk = (size_t)io.bk[k];
+      const double* dsrc[3] = {io.dxs[k], io.dus[k], io.dK[k]};
+      for (int i = 0; i < 3; ++i) {
+        const hipError_t e = hipMemcpyAsync((char*)hout[i] + b0 * per[6 + i], dsrc[i], bk * per[6 + i],
+                                            hipMemcpyDefault, io.ss[k]);
+        if (e != hipSuccess)
+          return drain_host_solve(h, fail(h, FFDDP_E_DEVICE, std::string("hipMemcpyAsync: ") + hipGetErrorString(e)));
+      }
+      const hipError_t e = hipEventRecord(io.done[k], io.ss[k]);
+      if (e != hipSuccess)
+        return drain_host_solve(h, fail(h, FFDDP_E_DEVICE, std::string("hipEventRecord: ") + hipGetErrorString(e)));
+    }
+  }
+  const double t3 = tm ? now() : 0.0;
+  // drain the slices in the order they finish
   double tw[8] = {0}, tc[8] = {0};
-  for (int k = 0; k < io.ns; ++k) {
-    const hipError_t e = hipEventSynchronize(io.done[k]);
-    if (e != hipSuccess)
-      return drain_host_solve(h, fail(h, FFDDP_E_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(e)));
+  bool drained[8] = {false};
+  for (int left = io.ns; left > 0;) {
+    int k = -1;
+    for (int j = 0; j < io.ns && k < 0; ++j) {
+      if (drained[j]) continue;
+      const hipError_t e = hipEventQuery(io.done[j]);
+      if (e == hipSuccess) k = j;
+      else if (e != hipErrorNotReady)
+        return drain_host_solve(h, fail(h, FFDDP_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e)));
+    }
+    if (k < 0) {
+      std::this_thread::yield();
+      continue;
+    }
     if (tm) tw[k] = now();
-    jobs.clear();
+    std::vector<CopyJob> jobs;
     for (int i = 0; i < 8; ++i) {
       if (!staged[i]) continue;
       const size_t o = (size_t)io.b0[k] * per[6 + i];
       jobs.push_back(CopyJob{(char*)uout[i] + o, (const char*)hout[i] + o, (size_t)io.bk[k] * per[6 + i]});
     }
-    host_copy(jobs);
+    pool.run(jobs);
     if (tm) tc[k] = now();
+    drained[k] = true;
+    --left;
   }
   {
     const hipError_t e = hipStreamSynchronize(cs);
@@ -3250,7 +3466,9 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
       return drain_host_solve(h, fail(h, FFDDP_E_DEVICE, std::string("hipStreamSynchronize: ") + hipGetErrorString(e)));
   }
   if (tm) {
-    std::fprintf(stderr, "[ffddp host io] stage-in %.2f ms, enqueue %.2f ms", t1 - t0, t2 - t1);
+    std::fprintf(stderr, "[ffddp host io] %d copy threads | enqueue+stage-in %.2f ms", pool.threads(), t2 - t0);
+    for (int k = 0; k < io.ns; ++k) std::fprintf(stderr, " (slice %d staged +%.2f)", k, tst[k] - t0);
+    std::fprintf(stderr, " | output first touch done +%.2f", t3 - t0);
     for (int k = 0; k < io.ns; ++k) std::fprintf(stderr, " | slice %d done +%.2f copied +%.2f", k, tw[k] - t0, tc[k] - t0);
     std::fprintf(stderr, " | total %.2f ms\n", now() - t0);
   }

@@ -17,6 +17,7 @@ per-iteration record of instance 0 after each solve (ffddp.callbacks).
 from __future__ import annotations
 
 import ctypes as C
+import threading
 import weakref
 
 import numpy as np
@@ -33,16 +34,92 @@ _PARAMS = ("th_stop", "th_grad", "th_acceptstep", "th_acceptnegstep", "th_stepde
            "reg_max", "reg_incfactor", "reg_decfactor", "neg_step_rule")
 
 
+class _RecycledPinned:
+    """Page-locked host blocks (ffddp_host_alloc) for solve()'s output arrays,
+    recycled instead of freed: every solve() returns fresh arrays (no other
+    live array shares their memory), and when the last array viewing a block
+    is gone (weakref finalizer) the block goes back to the free list rather
+    than to the allocator.  In steady state a solve then neither faults in
+    nor unmaps ~118 MB of output pages (B = 4096), and ffddp_solve_batch
+    copies into them by DMA as each slice finishes (no staging copy).  At
+    most `cap` bytes are page-locked; past that solve() falls back to plain
+    numpy arrays."""
+
+    def __init__(self, cap: int):
+        self.cap = int(cap)
+        self.total = 0
+        self.free = {}  # nbytes -> [addresses]
+        self.closed = False
+        self.lock = threading.Lock()
+
+    def arrays(self, specs):
+        offs, tot = {}, 0
+        for k, (shape, dt) in specs.items():
+            offs[k] = tot
+            tot += (int(np.prod(shape)) * np.dtype(dt).itemsize + 255) // 256 * 256
+        tot = max(tot, 1)
+        with self.lock:
+            lst = self.free.get(tot)
+            p = lst.pop() if lst else None
+            if p is None and self.total + tot <= self.cap:
+                self.total += tot
+                p = -1
+        if p is None:
+            return None
+        if p == -1:
+            q = C.c_void_p()
+            if _abi.load().ffddp_host_alloc(tot, C.byref(q)) != 0:
+                with self.lock:
+                    self.total -= tot
+                return None
+            p = q.value
+        buf = (C.c_char * tot).from_address(p)
+        weakref.finalize(buf, self._give_back, tot, p)
+        return {k: np.frombuffer(buf, dtype=dt, count=int(np.prod(shape)), offset=offs[k]).reshape(shape)
+                for k, (shape, dt) in specs.items()}
+
+    def _give_back(self, tot, p):
+        with self.lock:
+            if not self.closed:
+                self.free.setdefault(tot, []).append(p)
+                return
+            self.total -= tot
+        _abi.load().ffddp_host_free(C.c_void_p(p))
+
+    def close(self):
+        with self.lock:
+            self.closed = True
+            blocks = [(t, p) for t, lst in self.free.items() for p in lst]
+            self.free = {}
+            self.total -= sum(t for t, _ in blocks)
+        lib = _abi.load()
+        for _, p in blocks:
+            lib.ffddp_host_free(C.c_void_p(p))
+
+
 class BatchedBoxFDDP:
-    def __init__(self, cfg: OcpConfig, max_batch: int, device: int = 0, pinned_outputs: bool = False):
-        """pinned_outputs: solve() writes xs / us / K / ... into page-locked
-        arrays owned by the solver (copied by DMA as each slice finishes)
-        and returns views of them, overwritten by the next solve() -- copy
-        what must outlive it, as the reference does (crocoddyl_classical.py:
-        382-385).  Default: fresh arrays per solve()."""
+    def __init__(self, cfg: OcpConfig, max_batch: int, device: int = 0, pinned_outputs: bool = False,
+                 outputs: str | None = None):
+        """outputs: how solve() returns xs / us / K / cost / ...:
+          "recycled" (default): fresh numpy arrays per solve() in page-locked
+              memory recycled from earlier solves whose arrays are gone
+              (_RecycledPinned; up to 4 solves' worth at max_batch), filled by
+              DMA as each slice finishes;
+          "fresh": fresh pageable numpy arrays per solve() (np.zeros, filled
+              through the library's staging buffer);
+          "pinned" (or pinned_outputs=True): page-locked arrays owned by the
+              solver and overwritten by the next solve() -- copy what must
+              outlive it, as the reference does (crocoddyl_classical.py:
+              382-385)."""
         self.cfg = cfg
-        self.pinned_outputs = bool(pinned_outputs)
+        if outputs is None:
+            outputs = "pinned" if pinned_outputs else "recycled"
+        if outputs not in ("recycled", "fresh", "pinned"):
+            raise ValueError(f"outputs={outputs!r}")
+        self.outputs = outputs
+        self.pinned_outputs = outputs == "pinned"
         self._pin = {}
+        self._pool = None
         self._callbacks = []
         self._trace_it = 0
         self._plans = weakref.WeakSet()  # live SolvePlans: closed before the handle
@@ -60,6 +137,10 @@ class BatchedBoxFDDP:
             raise FfddpError(f"ffddp_create failed with code {rc}")
         self._h = h
         self.xs = self.us = self.K = self.cost = self.iter = self.ok = self.fn_pred = self.stats = None
+        if outputs == "recycled":
+            N, nx, Bm = self.N, self.nx, self.max_batch
+            one = 8 * Bm * ((N + 1) * nx + N * 7 + N * 7 * nx + 1 + 2) + 4 * Bm * (1 + _abi.NSTATS) + Bm + 8 * 256
+            self._pool = _RecycledPinned(4 * one)
 
     # -- solver properties (crocoddyl SolverFDDP / SolverBoxFDDP attributes) ----------
     @property
@@ -123,6 +204,8 @@ class BatchedBoxFDDP:
     def close(self):
         for plan in list(getattr(self, "_plans", ())):
             plan.close()
+        if getattr(self, "_pool", None) is not None:
+            self._pool.close()
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.ffddp_destroy(self._h)
             self._h = None
@@ -171,11 +254,14 @@ class BatchedBoxFDDP:
         specs = dict(xs=((B, N + 1, nx), np.float64), us=((B, N, 7), np.float64), K=((B, N, 7, nx), np.float64),
                      cost=((B,), np.float64), iters=((B,), np.int32), ok=((B,), np.uint8), fn=((B, 2), np.float64),
                      stats=((B, _abi.NSTATS), np.int32))
-        if self.pinned_outputs:
+        o = None
+        if self.outputs == "pinned":
             if B not in self._pin:
                 self._pin = {B: _abi.pinned_arrays(specs)}
             o = self._pin[B]
-        else:
+        elif self.outputs == "recycled":
+            o = self._pool.arrays(specs)
+        if o is None:
             o = {k: np.zeros(shape, dt) for k, (shape, dt) in specs.items()}
         xs, us, K, cost, iters, ok, fn, stats = (o[k] for k in ("xs", "us", "K", "cost", "iters", "ok", "fn", "stats"))
         d, i, u = _abi.dptr, _abi.iptr, _abi.uptr

@@ -97,19 +97,35 @@ def test_full_batch_equals_small_batches(variant, B, regime, monkeypatch):
 
 def test_pinned_outputs_bit_identical():
     """Host entry point with page-locked caller arrays (DMA per slice, no
-    staging) vs pageable ones (staging buffer + host copies): same bits."""
+    staging) vs pageable ones (staging buffer, first touch during the solve,
+    host copies as slices finish) vs the default recycled page-locked outputs:
+    same bits.  Recycled outputs are fresh per call while the caller holds
+    the previous ones, and reused once they are gone."""
     N, B = 30, 1030
     cfg = product_cfg("classical", N)
     batch = make_batch("classical", B, N, seed=78)
-    a = BatchedBoxFDDP(cfg, max_batch=B)
+    a = BatchedBoxFDDP(cfg, max_batch=B, outputs="fresh")
     a.solve(batch, maxiter=10)
     p = BatchedBoxFDDP(cfg, max_batch=B, pinned_outputs=True)
     p.solve(batch, maxiter=10)
+    r = BatchedBoxFDDP(cfg, max_batch=B)
+    assert r.outputs == "recycled"
+    r.solve(batch, maxiter=10)
     for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred", "stats"):
         assert np.array_equal(getattr(a, name), getattr(p, name), equal_nan=True), name
+        assert np.array_equal(getattr(a, name), getattr(r, name), equal_nan=True), name
     first = p.xs
     p.solve(batch.slice(slice(0, B)), maxiter=10)  # same buffers, overwritten in place
     assert p.xs is first
+    # recycled: the held result keeps its block; a second solve gets another
+    held_xs, held_K = r.xs, r.K
+    r.solve(batch, maxiter=10)
+    assert not np.shares_memory(held_xs, r.xs) and not np.shares_memory(held_K, r.K)
+    assert np.array_equal(held_xs, r.xs) and np.array_equal(held_K, r.K)
+    addr = held_xs.ctypes.data
+    del held_xs, held_K
+    r.solve(batch, maxiter=10)  # the released block comes back
+    assert r.xs.ctypes.data == addr
     # page-locked inputs as well (per-slice DMA of the inputs, no staging)
     pin = p.pinned_batch(batch)
     p.solve(pin, maxiter=10)
@@ -117,6 +133,7 @@ def test_pinned_outputs_bit_identical():
         assert np.array_equal(getattr(a, name), getattr(p, name), equal_nan=True), name
     a.close()
     p.close()
+    r.close()
 
 
 def test_feasible_warm_start_matches_oracle():

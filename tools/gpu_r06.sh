@@ -14,9 +14,14 @@ cd $R
 STEPS=${STEPS:-"tests bench"}
 for st in $STEPS; do
   case $st in
-    hostio) HOSTIO_CONFIGS=${HOSTIO_CONFIGS:-pageable:0,pinned:0} timeout -k 10 200 python3 tools/hostio.py 4096 ${HOSTIO_REPS:-5} \
-              > $O/hostio.txt 2>&1 || { tail -20 $O/hostio.txt; exit 1; }
-            grep -v amdgpu.ids $O/hostio.txt | tail -14 | cut -c1-400 ;;
+    hostio) for L in ${HOSTIO_LIBS:-base main}; do
+              if [ $L = main ]; then LIB=$R/franka-force-feedback-mpc_amd/lib/libffddp.so; else LIB=$R/franka-force-feedback-mpc_amd/lib/$L/libffddp.so; fi
+              FFDDP_LIB=$LIB HOSTIO_CONFIGS=${HOSTIO_CONFIGS:-pageable:0,pinned:0} timeout -k 10 200 python3 tools/hostio.py 4096 ${HOSTIO_REPS:-5} \
+                > $O/hostio_$L.txt 2>&1 || { tail -20 $O/hostio_$L.txt; exit 1; }
+              echo "== $L"; grep -v amdgpu.ids $O/hostio_$L.txt | tail -14 | cut -c1-600
+            done ;;
+    probe) timeout -k 10 200 python3 tools/hostio_probe.py 4096 6 > $O/probe.txt 2>&1 || { tail -20 $O/probe.txt; exit 1; }
+           grep -v amdgpu.ids $O/probe.txt ;;
     avail) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --list-avail > $O/avail.txt 2>&1) || { tail -5 $O/avail.txt; exit 1; }
            grep -o -E "SQ_[A-Z0-9_]*(THREAD|LANE|ACTIVE|VALU)[A-Z0-9_]*" $O/avail.txt | sort -u | tr '\n' ' '; echo ;;
     lanes) BENCH_ARGS="${LANE_ARGS:---batch 4096}" bash $R/tools/pmc_lanes.sh $TAG/lanes > $O/lanes.log 2>&1 || { tail -20 $O/lanes.log; exit 1; }

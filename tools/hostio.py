@@ -1,6 +1,7 @@
 """Host entry point timing (ffddp_solve_batch) next to the device-resident
 entry point (ffddp_solve_batch_dev) on the same handle, at the metric's
-B = 4096: pageable vs page-locked output arrays.  FFDDP_HOSTIO_TIMING=1
+B = 4096: recycled page-locked output arrays (the default), fresh pageable
+ones (names "fresh*" / "pageable*"), solver-owned page-locked ones ("pinned*").  FFDDP_HOSTIO_TIMING=1
 makes the library print stage-in / enqueue / per-slice done and copied times
 to stderr.  usage: python tools/hostio.py [B] [reps]"""
 import os
@@ -29,10 +30,17 @@ T = dict(x0=torch.tensor(b.x0, **f64), node_ref=torch.tensor(b.node_ref, **f64),
          iters=torch.zeros(B, dtype=torch.int32, device="cuda"), ok=torch.zeros(B, dtype=torch.uint8, device="cuda"),
          fn_pred=torch.zeros((B, 2), **f64), stats=torch.zeros((B, _abi.NSTATS), dtype=torch.int32, device="cuda"))
 stream = torch.cuda.current_stream().cuda_stream
+# name:dbg[:ENV=VAL...]  (e.g. pageable_reg:0:FFDDP_HOSTIO_REGISTER=1)
 configs = [c.split(":") for c in (os.environ.get("HOSTIO_CONFIGS") or "pageable:0,pinned:0").split(",")]
-for name, dbg in configs:
+for name, dbg, *envs in configs:
     os.environ["FFDDP_HOSTIO_DBG"] = dbg
-    s = BatchedBoxFDDP(cfg, max_batch=B, pinned_outputs=name.startswith("pinned"))
+    for k in ("FFDDP_HOSTIO_REGISTER", "FFDDP_COPY_THREADS"):
+        os.environ.pop(k, None)
+    for e in envs:
+        k, v = e.split("=", 1)
+        os.environ[k] = v
+    outputs = "pinned" if name.startswith("pinned") else ("fresh" if name.startswith(("fresh", "pageable")) else "recycled")
+    s = BatchedBoxFDDP(cfg, max_batch=B, outputs=outputs)
     s.solve(b)
     s.solve_dev(T, stream=stream)
     torch.cuda.synchronize()
