@@ -139,7 +139,16 @@ def sq_limiter(variant, contact, B, N):
         return None
     if j.get("config") != f"{variant}/{contact}/B{B}/N{N}":
         return None
-    return {"source": j.get("source"), "summary": j.get("summary"), "kernels": j.get("kernels")}
+    out = {"source": j.get("source"), "summary": j.get("summary"), "kernels": j.get("kernels")}
+    # VALU lane utilisation per kernel (tools/pmc_lanes.sh -> profiles/lanes_latest.json: the mean fraction of
+    # a wave's 64 lanes enabled while it issues VALU instructions, SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU
+    # normalised by a 64-lane calibration kernel)
+    lj = _profile_json("lanes_latest.json", variant, contact, B, N)
+    if lj:
+        out["lane_utilisation"] = {k: v.get("lane_util") for k, v in lj.get("kernels", {}).items()
+                                   if v.get("lane_util") is not None}
+        out["lane_source"] = lj.get("source")
+    return out
 
 
 def _profile_json(name, variant, contact, B, N):

@@ -1989,15 +1989,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROW ? 1 : FW
   };
   fetch(0);
   for (int t = 0; t <= N; ++t) {
-    // the lane predicates, recomputed per node from an opaque lane index
-    // (kept across the loop they are scalar-register masks that spill;
-    // ffddp_rollout.hpp FFDDP_LS_OPAQUE_LANE)
-#if FFDDP_LS_OPAQUE_LANE
-    int lt = (int)threadIdx.x;
-    asm volatile("" : "+v"(lt));
-    const bool J = (lt & (G8 - 1)) < NQ;
-    const bool Js = J && (!ROW || (lt & 8) == 0);
-#endif
     double xq_t = hq, xv_t = hv, xt_t = ht;
     const double sq = pxs[0], sv = pxs[1], stt = pxs[2];
     if (gap) {

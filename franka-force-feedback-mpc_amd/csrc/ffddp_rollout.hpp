@@ -27,11 +27,6 @@
 
 #pragma clang fp contract(off)
 
-// lane index opaque per node (1) or hoisted by the compiler (0)
-#ifndef FFDDP_LS_OPAQUE_LANE
-#define FFDDP_LS_OPAQUE_LANE 1
-#endif
-
 // the rollout's contact solve: one backward substitution through the Schur
 // complement (1) or two solves (0)
 #ifndef FFDDP_LS_SCHUR
@@ -252,15 +247,7 @@ __device__ __forceinline__ void ls_node_calc(const DevConsts& C, unsigned fl, co
                                              , unsigned long long (&pp_acc)[12], unsigned long long& pp_last
 #endif
 ) {
-  // the lane index, opaque per node: the lane masks derived from it (li == k,
-  // li >= d, J, ...) are then recomputed where they are used (one v_cmp each)
-  // instead of hoisted out of the node loop and kept in scalar register
-  // pairs, which overflowed the scalar file into VGPR-lane spills (two
-  // v_readlane per restored mask, inside the loop)
-  int li = g8_lane();
-#if FFDDP_LS_OPAQUE_LANE
-  asm volatile("" : "+v"(li));
-#endif
+  const int li = g8_lane();
   const bool J = li < NQ;
   const bool with_dyn = mode != MODE_TERMINAL_X;
   const bool terminal = mode != MODE_RUNNING;
