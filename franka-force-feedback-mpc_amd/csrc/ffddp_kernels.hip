@@ -2458,7 +2458,12 @@ struct CopyJob {
 class CopyPool {
  public:
   explicit CopyPool(int nthreads) {
-    for (int i = 1; i < nthreads; ++i) th_.emplace_back([this] { worker(); });
+    // no exception may cross the C ABI: with fewer threads than asked (or
+    // none) the calling thread does the rest of the copies
+    try {
+      for (int i = 1; i < nthreads; ++i) th_.emplace_back([this] { worker(); });
+    } catch (...) {
+    }
   }
   ~CopyPool() {
     {
@@ -3311,7 +3316,13 @@ int ffddp_solve_batch(ffddp_handle* h, int B, const double* x0, const double* no
     HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     h->hdone.push_back(e);
   }
-  if (!h->pool) h->pool = new (std::nothrow) CopyPool(copy_threads());
+  if (!h->pool) {
+    try {
+      h->pool = new CopyPool(copy_threads());
+    } catch (...) {
+      h->pool = nullptr;
+    }
+  }
   if (!h->pool) return fail(h, FFDDP_E_OOM, "copy pool");
   CopyPool& pool = *h->pool;
   HostIO io;
