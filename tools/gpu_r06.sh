@@ -23,6 +23,8 @@ for st in $STEPS; do
     probe) timeout -k 10 200 python3 tools/hostio_probe.py 4096 6 > $O/probe.txt 2>&1 || { tail -20 $O/probe.txt; exit 1; }
            grep -v amdgpu.ids $O/probe.txt ;;
     rehearse) bash $R/tools/rehearse_multi.sh $TAG/rehearse ;;
+    phase) for spec in "1 tracking" "1 random" "1024 random"; do set -- $spec; echo "== prof B=$1 $2"
+             FFDDP_LIB=$R/franka-force-feedback-mpc_amd/lib/prof/libffddp.so timeout -k 10 200 python3 tools/phase_prof.py $1 classical "" $2 2>&1 | grep -v amdgpu.ids; done | tee $O/phase_prof.txt ;;
     avail) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --list-avail > $O/avail.txt 2>&1) || { tail -5 $O/avail.txt; exit 1; }
            grep -o -E "SQ_[A-Z0-9_]*(THREAD|LANE|ACTIVE|VALU)[A-Z0-9_]*" $O/avail.txt | sort -u | tr '\n' ' '; echo ;;
     lanes) BENCH_ARGS="${LANE_ARGS:---batch 4096}" bash $R/tools/pmc_lanes.sh $TAG/lanes > $O/lanes.log 2>&1 || { tail -20 $O/lanes.log; exit 1; }

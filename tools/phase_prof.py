@@ -12,11 +12,12 @@ from ffddp.config import classical_preset, ff_preset
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 variant = sys.argv[2] if len(sys.argv) > 2 else "classical"
-names = sys.argv[3].split(",") if len(sys.argv) > 3 else [f"p{i}" for i in range(8)]
+names = sys.argv[3].split(",") if len(sys.argv) > 3 and sys.argv[3] else [f"p{i}" for i in range(8)]
+regime = sys.argv[4] if len(sys.argv) > 4 else "tracking"
 N = 30
 cfg = ff_preset(N) if variant == "ff" else classical_preset(N)
 ee = R.R_MJ_FROM_PIN @ _abi.frame_placement(R.Q_NEUTRAL)[1]
-b = workload.make_batch(B, N, variant, _abi.gravity_torque, ee, seed=1234, fk=_abi.frame_placement)
+b = workload.make_batch(B, N, variant, _abi.gravity_torque, ee, seed=1234, regime=regime, fk=_abi.frame_placement)
 s = BatchedBoxFDDP(cfg, max_batch=B)
 lib = _abi.load()
 f = lib.ffddp_debug_phase_read
