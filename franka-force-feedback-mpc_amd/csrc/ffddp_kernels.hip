@@ -799,7 +799,10 @@ __device__ __forceinline__ bool lane0(bool c) { return (__ballot(c) & 1ull) != 0
 // norm are lane-local terms summed / maxed by DPP over the 8 lanes; only the
 // vectors a mat-vec needs (x, the trial point) are broadcast.
 __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&hrow)[NU], double q, double lb,
-                                            double ub, double& x, double (&Lr)[NU], int& clmask, int lane) {
+                                            double ub, double& x, double (&Lr)[NU], int& clmask, int lane,
+                                            unsigned long long* pq = nullptr) {
+  (void)pq;  // FFDDP_PHASE_PROF builds: the split of this QP's time (BQ_*)
+  BQ_T0();
   x = fmax(fmin(x, ub), lb);
   bool have = false, cl = false;
   double xsf = 0.0;
@@ -819,6 +822,8 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
     const bool c = (x == lb && g > 0.0) || (x == ub && g < 0.0);
     const bool changed = !have || ((__ballot(c != cl) & 0x7Full) != 0);
     cl = c;
+    BQ_CNT(6);
+    BQ_ACC(0);
     if (changed) {
       const int m = (int)(__ballot(cl) & 0x7Full);
 #pragma unroll
@@ -827,6 +832,8 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
         Lr[j] = (!cl && !cj) ? hrow[j] + (lane == j ? C.qp_reg : 0.0) : (lane == j ? 1.0 : 0.0);
       }
       if (!chol_rows(Lr, lane)) return false;
+      BQ_CNT(7);
+      BQ_ACC(1);
       have = true;
       double r = -q;
 #pragma unroll
@@ -834,9 +841,14 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
         if ((m >> j) & 1) r -= hrow[j] * xb[j];
       xsf = chol_solve_rows(Lr, cl ? 0.0 : r, lane);
       clmask = m;
+      BQ_ACC(2);
     }
     const double dx = cl ? 0.0 : xsf - x;
-    if (lane0(max8(fabs(dx)) < C.qp_th_grad)) break;
+    if (lane0(max8(fabs(dx)) < C.qp_th_grad)) {
+      BQ_ACC(3);
+      break;
+    }
+    BQ_ACC(3);
     bool moved = false;
 #pragma unroll 1
     for (int ia = 0; ia < NTRIALS; ++ia) {
@@ -860,13 +872,18 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
     // ~1 QP in 3700 stalls this way (numpy oracle, tests/golden/
     // make_boxqp_stagnation.py), and its ~90 repeated iterations (10 trials
     // each) set the backward launch's tail.
+    BQ_ACC(4);
     if (!moved) break;
     // The next iteration's convergence test without its mat-vec: with no
     // control clamped now and none at a bound after the step, that
     // iteration's clamped set is empty again (no refactor, same xsf) and its
     // step is dx = xsf - x, so when that is below th_grad it stops right
     // there with this x.  (Otherwise it runs as usual.)
-    if (!(__ballot(cl || x == lb || x == ub) & 0x7Full) && lane0(max8(fabs(xsf - x)) < C.qp_th_grad)) break;
+    if (!(__ballot(cl || x == lb || x == ub) & 0x7Full) && lane0(max8(fabs(xsf - x)) < C.qp_th_grad)) {
+      BQ_ACC(5);
+      break;
+    }
+    BQ_ACC(5);
   }
   return true;
 }
@@ -1621,7 +1638,14 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const double ub = v ? S.uub[l % NU] - S.uu[l % NU] : 0.0;
           double x = v ? S.kp[l % NU] : 0.0;
           int clm = 0;
+#ifdef FFDDP_PHASE_PROF
+          unsigned long long bq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l, b == 0 ? bq : nullptr);
+          if (b == 0 && l == 0)
+            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_pp[32 + k_], bq[k_]);
+#else
           ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l);
+#endif
           if (ok && v) {
             const bool c = (clm >> l) & 1;
             S.kk[l] = -x;
@@ -3183,9 +3207,9 @@ int ffddp_create(const ffddp_robot* robot, const ffddp_ocp_config* cfg, int devi
 
 #ifdef FFDDP_PHASE_PROF
 extern "C" int ffddp_debug_phase_read(unsigned long long* out, int n, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ffddp::g_pp), sizeof(unsigned long long) * (n < 32 ? n : 32)) != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ffddp::g_pp), sizeof(unsigned long long) * (n < 48 ? n : 48)) != hipSuccess) return -2;
   if (reset) {
-    unsigned long long z[32] = {0};
+    unsigned long long z[48] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(ffddp::g_pp), z, sizeof(z)) != hipSuccess) return -2;
   }
   return 0;

@@ -22,11 +22,11 @@ s = BatchedBoxFDDP(cfg, max_batch=B)
 lib = _abi.load()
 f = lib.ffddp_debug_phase_read
 f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
-buf = (C.c_ulonglong * 32)()
+buf = (C.c_ulonglong * 48)()
 s.solve(b, maxiter=10)
-f(buf, 32, 1)
+f(buf, 48, 1)
 s.solve(b, maxiter=10)
-f(buf, 32, 1)
+f(buf, 48, 1)
 st = s.stats[0]
 nodes = int(st[3]) * N  # backward passes x nodes
 print("instance 0: iters", s.iter[0], "backward passes", st[3], "forward passes", st[5])
@@ -43,3 +43,9 @@ if buf[28] or buf[29]:
     bnodes = int(st[3]) * N
     print(f"  bw2 phase D, wave 0 (gains)      {buf[28] / max(1, bnodes):10.0f} cycles/node")
     print(f"  bw2 phase D, wave 1 (stage + spec) {buf[29] / max(1, bnodes):10.0f} cycles/node")
+if any(buf[32 + i] for i in range(8)):
+    bnodes = int(st[3]) * N
+    its, facts = buf[38], buf[39]
+    print(f"  BoxQP (two-wave backward, instance 0): {its / max(1, bnodes):.2f} iterations and {facts / max(1, bnodes):.2f} factorisations per node")
+    for i, n in enumerate(["gradient+fold+set", "factorisation", "solve", "convergence test", "line search", "early-exit test"]):
+        print(f"    {n:20s} {buf[32 + i] / max(1, bnodes):8.0f} cycles/node")
