@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from ffddp import BatchedBoxFDDP, FfddpError
+from ffddp import BatchedBoxFDDP, FfddpError, _abi
 
 from helpers import elem_err, log_parity, make_batch, oracle_cfg, oracle_problem, oracle_solve, product_cfg, rel_err
 from oracle_pool import solve_many
@@ -134,6 +134,45 @@ def test_pinned_outputs_bit_identical():
     a.close()
     p.close()
     r.close()
+
+
+def test_host_output_modes_bit_identical(monkeypatch):
+    """The host entry point's output paths at a multi-slice and a one-slice
+    batch: fresh pageable outputs (staging buffer), outputs page-locked for the
+    call (FFDDP_HOSTIO_REGISTER=1, read at each call) and recycled page-locked
+    outputs give the same bits as the device entry point."""
+    import torch
+
+    for B in (300, 100):
+        N = 30
+        cfg = product_cfg("classical", N)
+        batch = make_batch("classical", B, N, seed=79 + B)
+        dev = torch.device("cuda", 0)
+        f64 = dict(dtype=torch.float64, device=dev)
+        t = dict(x0=torch.tensor(batch.x0, **f64), node_ref=torch.tensor(batch.node_ref, **f64),
+                 inst_ref=torch.tensor(batch.inst_ref, **f64),
+                 surface=torch.tensor(batch.surface, dtype=torch.uint8, device=dev),
+                 xs_init=torch.tensor(batch.xs_init, **f64), us_init=torch.tensor(batch.us_init, **f64),
+                 xs=torch.zeros((B, N + 1, 14), **f64), us=torch.zeros((B, N, 7), **f64),
+                 K=torch.zeros((B, N, 7, 14), **f64), cost=torch.zeros(B, **f64),
+                 iters=torch.zeros(B, dtype=torch.int32, device=dev), ok=torch.zeros(B, dtype=torch.uint8, device=dev),
+                 fn_pred=torch.zeros((B, 2), **f64), stats=torch.zeros((B, _abi.NSTATS), dtype=torch.int32, device=dev))
+        d = BatchedBoxFDDP(cfg, max_batch=B)
+        d.solve_dev(t, maxiter=10)
+        torch.cuda.synchronize(dev)
+        ref = {k: t[k].cpu().numpy() for k in ("xs", "us", "K", "cost", "stats")}
+        d.close()
+        for outputs, env in (("fresh", None), ("fresh", "1"), ("recycled", None)):
+            if env is None:
+                monkeypatch.delenv("FFDDP_HOSTIO_REGISTER", raising=False)
+            else:
+                monkeypatch.setenv("FFDDP_HOSTIO_REGISTER", env)
+            s = BatchedBoxFDDP(cfg, max_batch=B, outputs=outputs)
+            s.solve(batch, maxiter=10)
+            for k, v in ref.items():
+                assert np.array_equal(getattr(s, k), v, equal_nan=True), (B, outputs, env, k)
+            s.close()
+        monkeypatch.delenv("FFDDP_HOSTIO_REGISTER", raising=False)
 
 
 def test_feasible_warm_start_matches_oracle():
