@@ -780,16 +780,14 @@ __device__ __forceinline__ double chol_solve_rows(const double (&Lr)[NU], double
   return out;
 }
 
-// max over lanes 0..7 (lanes >= NU hold 0), in every lane of the group
-__device__ __forceinline__ double max8(double v) {
-  v = fmax(v, dpp64<0x141>(v));  // row_half_mirror
-  v = fmax(v, dpp64<0xB1>(v));   // quad_perm [1,0,3,2]
-  v = fmax(v, dpp64<0x4E>(v));   // quad_perm [2,3,0,1]
-  return v;
-}
 // a branch on lane 0's value of a condition (lane 0 holds the 8-lane sums /
 // maxima like every lane of its group): a ballot bit, no readlane round trip
 __device__ __forceinline__ bool lane0(bool c) { return (__ballot(c) & 1ull) != 0; }
+// max over lanes 0..7 of |v| below th, as one ballot instead of max8's three
+// DPP steps: the same decision (v_max_f64 skips a NaN operand and a NaN lane
+// fails `>= th` alike; lane 7 holds 0 in every BoxQP vector, so the maximum
+// is never taken over NaN lanes only)
+__device__ __forceinline__ bool all8_below(double av, double th) { return (__ballot(av >= th) & 0x7Full) == 0; }
 
 // crocoddyl::BoxQP::solve with variable i on lane i: projected Newton on the
 // free set, refactored when it changes, Armijo line search over the same
@@ -844,7 +842,7 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
       BQ_ACC(2);
     }
     const double dx = cl ? 0.0 : xsf - x;
-    if (lane0(max8(fabs(dx)) < C.qp_th_grad)) {
+    if (all8_below(fabs(dx), C.qp_th_grad)) {
       BQ_ACC(3);
       break;
     }
@@ -879,7 +877,7 @@ __device__ __forceinline__ bool boxqp_lanes(const DevConsts& C, const double (&h
     // iteration's clamped set is empty again (no refactor, same xsf) and its
     // step is dx = xsf - x, so when that is below th_grad it stops right
     // there with this x.  (Otherwise it runs as usual.)
-    if (!(__ballot(cl || x == lb || x == ub) & 0x7Full) && lane0(max8(fabs(xsf - x)) < C.qp_th_grad)) {
+    if (!(__ballot(cl || x == lb || x == ub) & 0x7Full) && all8_below(fabs(xsf - x), C.qp_th_grad)) {
       BQ_ACC(5);
       break;
     }
