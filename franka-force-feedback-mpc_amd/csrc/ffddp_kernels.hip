@@ -1624,6 +1624,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.QQ[QH + l * NU + j] : (l == j ? 1.0 : 0.0);
         bool ok;
+        int clm = 0;
         if (!use_qp) {
 #pragma unroll
           for (int j = 0; j < NU; ++j) Lr[j] = hrow[j];
@@ -1635,7 +1636,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const double lb = v ? S.ulb[l % NU] - S.uu[l % NU] : 0.0;
           const double ub = v ? S.uub[l % NU] - S.uu[l % NU] : 0.0;
           double x = v ? S.kp[l % NU] : 0.0;
-          int clm = 0;
 #ifdef FFDDP_PHASE_PROF
           unsigned long long bq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
           ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l, b == 0 ? bq : nullptr);
@@ -1655,7 +1655,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (int j = 0; j < NU; ++j)
             if (j <= l) S.sl.L[tri(l, j)] = Lr[j];
-        if (l == 0) S.flag = ok ? 1 : 0;
+        // ok, and the final clamped set above it (one LDS word for the tests below)
+        if (l == 0) S.flag = ok ? 1 | (clm << 1) : 0;
       } else {
         if (t > 0) {
 #pragma unroll
@@ -1716,16 +1717,13 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #endif
       lds_sync();
       PP(4);
-      if (S.flag == 0) {
+      const int dflag = S.flag;
+      if (dflag == 0) {
         failed = true;
         break;
       }
       // wave 1's gains stand unless BoxQP clamped a control
-      bool spec_ok = S.spec != 0;
-      if (use_qp) {
-#pragma unroll
-        for (int c = 0; c < NU; ++c) spec_ok = spec_ok && S.clamped[c] == 0;
-      }
+      const bool spec_ok = S.spec != 0 && (dflag >> 1) == 0;
       // ---- phase E: K columns (and k for LLT), wave 0 ----
       if (!spec_ok && wv == 0 && (l < NX || (!use_qp && l == NX))) {
         double col[NU];
