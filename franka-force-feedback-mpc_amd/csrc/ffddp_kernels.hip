@@ -622,7 +622,6 @@ template <bool FF> struct BwW {
   double fsb[2][BW_DIET_SLOTS ? NX : 64];  // k_backward_w2: node t's gap in slot t & 1 (staged before node t+1's phase G reads its own)
   int flag;
   int badw[2];  // k_backward_w2: per-wave NaN flags of phases F / G
-  int clamped[NU];
 #ifdef BW_PAD_CL
   double pad[FF ? 1 : BW_PAD_CL];  // development: classical LDS footprint back to the round-4 size
 #endif
@@ -1132,6 +1131,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       lds_sync();
       PP(3);
       // ---- phase D: gains (Eigen::LLT or BoxQP), row / variable i on lane i ----
+      int clm = 0;  // the final clamped set (uniform: phase E runs on this wave)
       {
         double hrow[NU], Lr[NU];
 #pragma unroll
@@ -1141,19 +1141,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 #pragma unroll
           for (int j = 0; j < NU; ++j) Lr[j] = hrow[j];
           ok = chol_rows(Lr, l);
-          if (l < NU) S.clamped[l] = 0;
         } else {
           const bool v = l < NU;
           const double q = v ? S.Qv[NX + l] : 0.0;
           const double lb = v ? S.ulb[l % NU] - S.uu[l % NU] : 0.0;
           const double ub = v ? S.uub[l % NU] - S.uu[l % NU] : 0.0;
           double x = v ? S.kp[l % NU] : 0.0;
-          int clm = 0;
           ok = boxqp_lanes(C, hrow, q, lb, ub, x, Lr, clm, l);
           if (ok && v) {
             const bool c = (clm >> l) & 1;
             S.kk[l] = -x;
-            S.clamped[l] = c ? 1 : 0;
             if (c) S.Qv[NX + l] = 0.0;  // BoxFDDP: clamped Qu entries are zeroed
           }
         }
@@ -1178,7 +1175,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
         double col[NU];
         if (l < NX) {
 #pragma unroll
-          for (int c = 0; c < NU; ++c) col[c] = S.clamped[c] ? 0.0 : S.QQ[QXU + l * NU + c];
+          for (int c = 0; c < NU; ++c) col[c] = ((clm >> c) & 1) ? 0.0 : S.QQ[QXU + l * NU + c];
         } else {
 #pragma unroll
           for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
@@ -1629,7 +1626,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (int j = 0; j < NU; ++j) Lr[j] = hrow[j];
           ok = chol_rows(Lr, l);
-          if (l < NU) S.clamped[l] = 0;
         } else {
           const bool v = l < NU;
           const double q = v ? S.Qv[NX + l] : 0.0;
@@ -1647,7 +1643,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
           if (ok && v) {
             const bool c = (clm >> l) & 1;
             S.kk[l] = -x;
-            S.clamped[l] = c ? 1 : 0;
             if (c) S.Qv[NX + l] = 0.0;  // BoxFDDP: clamped Qu entries are zeroed
           }
         }
@@ -1729,7 +1724,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         double col[NU];
         if (l < NX) {
 #pragma unroll
-          for (int c = 0; c < NU; ++c) col[c] = S.clamped[c] ? 0.0 : S.QQ[QXU + l * NU + c];
+          for (int c = 0; c < NU; ++c) col[c] = ((dflag >> (1 + c)) & 1) ? 0.0 : S.QQ[QXU + l * NU + c];
         } else {
 #pragma unroll
           for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
