@@ -779,6 +779,18 @@ __device__ __forceinline__ double chol_solve_rows(const double (&Lr)[NU], double
   return out;
 }
 
+// phase E's factor without the LDS round trip: the lower triangle of the
+// chol_rows factor (rows on lanes 0..6) in tri layout in every lane of DPP
+// row 0 (lanes 0..15: the classical pass's K columns and k), by row_newbcast.
+// chol_solve then reads the same values it would read from the LDS copy.
+constexpr bool e_from_regs(int nx) { return nx + 1 <= 16; }
+__device__ __forceinline__ void rows_to_tri(const double (&Lr)[NU], double (&Lt)[NU * (NU + 1) / 2]) {
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
+#pragma unroll
+    for (int k = 0; k <= i; ++k) Lt[tri(i, k)] = rowb(Lr[k], i);
+}
+
 // a branch on lane 0's value of a condition (lane 0 holds the 8-lane sums /
 // maxima like every lane of its group): a ballot bit, no readlane round trip
 __device__ __forceinline__ bool lane0(bool c) { return (__ballot(c) & 1ull) != 0; }
@@ -1132,8 +1144,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       PP(3);
       // ---- phase D: gains (Eigen::LLT or BoxQP), row / variable i on lane i ----
       int clm = 0;  // the final clamped set (uniform: phase E runs on this wave)
+      constexpr bool EREG = e_from_regs(NX);
+      double Lr[NU];  // the factor (EREG: read by phase E from these registers)
       {
-        double hrow[NU], Lr[NU];
+        double hrow[NU];
 #pragma unroll
         for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.QQ[QH + l * NU + j] : (l == j ? 1.0 : 0.0);
         bool ok;
@@ -1158,7 +1172,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
           failed = true;
           break;
         }
-        if (l < NU)
+        if (!EREG && l < NU)
 #pragma unroll
           for (int j = 0; j < NU; ++j)
             if (j <= l) S.sl.L[tri(l, j)] = Lr[j];
@@ -1180,7 +1194,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
 #pragma unroll
           for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
         }
-        chol_solve<NU>(S.sl.L, col);
+        if (EREG) {
+          double Lt[NU * (NU + 1) / 2];
+          rows_to_tri(Lr, Lt);
+          chol_solve<NU>(Lt, col);
+        } else {
+          chol_solve<NU>(S.sl.L, col);
+        }
         if (l < NX) {
 #pragma unroll
           for (int c = 0; c < NU; ++c) {
@@ -1616,8 +1636,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #endif
       // ---- phase D: gains on wave 0 (rows on lanes 0..6); wave 1 stages the
       // next node's record (S.R is not read after phase C) ----
+      constexpr bool EREG = e_from_regs(NX);
+      double Lr0[NU];  // wave 0's factor (EREG: read by phase E from these registers)
       if (wv == 0) {
-        double hrow[NU], Lr[NU];
+        double hrow[NU];
+        double (&Lr)[NU] = Lr0;
 #pragma unroll
         for (int j = 0; j < NU; ++j) hrow[j] = (l < NU) ? S.QQ[QH + l * NU + j] : (l == j ? 1.0 : 0.0);
         bool ok;
@@ -1646,7 +1669,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (c) S.Qv[NX + l] = 0.0;  // BoxFDDP: clamped Qu entries are zeroed
           }
         }
-        if (ok && l < NU)
+        if (!EREG && ok && l < NU)
 #pragma unroll
           for (int j = 0; j < NU; ++j)
             if (j <= l) S.sl.L[tri(l, j)] = Lr[j];
@@ -1729,7 +1752,13 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (int c = 0; c < NU; ++c) col[c] = S.Qv[NX + c];
         }
-        chol_solve<NU>(S.sl.L, col);
+        if (EREG) {
+          double Lt[NU * (NU + 1) / 2];
+          rows_to_tri(Lr0, Lt);
+          chol_solve<NU>(Lt, col);
+        } else {
+          chol_solve<NU>(S.sl.L, col);
+        }
         if (l < NX) {
           double* Kt = K_i + (unsigned)(t * NU * NX);
 #pragma unroll
