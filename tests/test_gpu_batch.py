@@ -95,6 +95,34 @@ def test_full_batch_equals_small_batches(variant, B, regime, monkeypatch):
     small.close()
 
 
+@pytest.mark.parametrize("B,regime", [(4096, "tracking"), (1024, "random")])
+def test_ff_full_batch_equals_small_batches_bits(B, regime, monkeypatch):
+    """FF bit-for-bit across batch shapes where the one-wave passes run
+    (B = 4096: the throughput and latency variants beside the two-wave tail)
+    and where BoxQP clamps controls (random x0: the gains' clamped set, phase
+    E after a clamp, the two-wave pass's flag word).  Bits only: the oracle
+    spread of FF is test_full_batch_equals_small_batches' FF case."""
+    N = 30
+    cfg = product_cfg("ff", N)
+    batch = make_batch("ff", B, N, seed=78, regime=regime)
+    big = BatchedBoxFDDP(cfg, max_batch=B)
+    big.solve(batch, maxiter=10)
+    monkeypatch.setenv("FFDDP_STREAMS", "1")
+    small = BatchedBoxFDDP(cfg, max_batch=8)
+    rng = np.random.default_rng(2)
+    picks = np.unique(np.concatenate([[0, B // 4, B // 2, B - 1], rng.integers(0, B, 12)]))
+    for i0 in range(0, len(picks), 8):
+        idx = picks[i0:i0 + 8]
+        small.solve(_sub(batch, idx), maxiter=10)
+        for j, i in enumerate(idx):
+            for name in ("xs", "us", "K", "cost", "iter", "ok", "fn_pred"):
+                assert np.array_equal(getattr(big, name)[i], getattr(small, name)[j], equal_nan=True), (name, int(i))
+            assert np.array_equal(big.stats[i][[0, 1, 2, 3, 4, 8, 9]], small.stats[j][[0, 1, 2, 3, 4, 8, 9]]), int(i)
+    assert np.all(np.isfinite(big.cost))
+    big.close()
+    small.close()
+
+
 def test_pinned_outputs_bit_identical():
     """Host entry point with page-locked caller arrays (DMA per slice, no
     staging) vs pageable ones (staging buffer, first touch during the solve,
