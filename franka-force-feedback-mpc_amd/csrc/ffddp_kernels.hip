@@ -1236,9 +1236,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LATE ? 1 : (
       // ---- phase G: Vx, gap terms, expected improvement, k ----
       double cdg = 0.0, cdq = 0.0, cst = 0.0;
       if (l < NX) {
+        // V fs (the gap term) only while infeasible: a feasible pass never
+        // reads it (uniform branch; FF computes it always: the branch costs
+        // its throughput pass a 12 B spill)
         double vfs = 0.0;
+        if (FF || !feas) {
 #pragma unroll
-        for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
+          for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * S.fs[i];
+        }
         double vx = S.Qv[l];
 #pragma unroll
         for (int c = 0; c < NU; ++c) vx -= S.sl.K[c * NX + l] * S.Qv[NX + c];
@@ -1470,8 +1475,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (l < NX) {
         double vfs = 0.0;
         const double* fsg = S.fsb[tg & 1];
+        if (FF || !feas) {  // the gap term only while infeasible (uniform branch)
 #pragma unroll
-        for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * fsg[i];
+          for (int i = 0; i < NX; ++i) vfs += S.V[i * NX + l] * fsg[i];
+        }
         double vx = S.Qv[l];
 #pragma unroll
         for (int c = 0; c < NU; ++c) vx -= S.sl.K[c * NX + l] * S.Qv[NX + c];
@@ -1519,6 +1526,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         pfs = fs_i[(unsigned)(tn * NX + lx)];
         pkp = k_i[(unsigned)(tn * NU + lu)];
         pus = us_i[(unsigned)(tn * NU + lu)];
+        PP(8);  // (profiling build: wave 0's staging apart from its phase G)
         if (t < N - 1) {
           phase_g(t + 1);
           // z below reads Vx entries other lanes of this wave just wrote

@@ -39,6 +39,8 @@ fnodes = int(st[5]) * (N + 1)
 tot = sum(buf[16 + i] for i in range(len(fw)))
 for i, n in enumerate(fw):
     print(f"  fw {n:10s} {buf[16 + i] / max(1, fnodes):10.0f} cycles/node  {100.0 * buf[16 + i] / max(1, tot):5.1f} %")
+if buf[8]:
+    print(f"  bw2 wave 0 staging (in 'stage') {buf[8] / max(1, int(st[3]) * N):10.0f} cycles/node")
 if buf[28] or buf[29]:
     bnodes = int(st[3]) * N
     print(f"  bw2 phase D, wave 0 (gains)      {buf[28] / max(1, bnodes):10.0f} cycles/node")
